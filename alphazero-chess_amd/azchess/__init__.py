@@ -1,0 +1,15 @@
+"""azchess -- MI355X-native self-play engine for AlexandreGac/alphazero-chess' MCTS+NN hot path.
+
+Host-side mirror of the reference's module surface (chess.rs, agent.rs, tree.rs,
+training.rs, parameters.rs) over the C-ABI of libaz.so (include/az.h).
+"""
+from . import _lib, parameters
+from .agent import AlphaZero, num_params, random_weights
+from .chess import (GameResult, GameState, IllegalMove, Position, index_to_move, move_to_index, play_move,
+                    to_tensor)
+from .training import EpisodeStep, SelfPlay, process_batch, run_all_episodes, run_episode
+from .tree import BatchedSearch, MCTree, make_cfg
+
+__all__ = ["AlphaZero", "num_params", "random_weights", "GameResult", "GameState", "IllegalMove", "Position",
+           "index_to_move", "move_to_index", "play_move", "to_tensor", "EpisodeStep", "SelfPlay", "process_batch",
+           "run_all_episodes", "run_episode", "BatchedSearch", "MCTree", "make_cfg", "parameters"]

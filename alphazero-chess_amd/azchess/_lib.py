@@ -1,0 +1,132 @@
+"""ctypes binding of libaz.so (include/az.h).
+
+The product path is libaz.so only: if the library is missing this module raises at import
+time -- there is no Python or CPU fallback for any compute entry point.
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libaz.so")
+CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
+
+ACTION_SPACE = 4096
+MAX_MOVES = 256
+ONGOING, DRAW, WHITE_WINS, BLACK_WINS, ILLEGAL = 0, 1, 2, 3, -1
+DTYPE_F32, DTYPE_BF16 = 0, 1
+EVAL_NET, EVAL_SYNTHETIC = 0, 1
+
+
+class AzPos(C.Structure):
+    _fields_ = [("bb", C.c_uint64 * 8), ("turn", C.c_uint8), ("castling", C.c_uint8), ("ep", C.c_uint8),
+                ("flags", C.c_uint8), ("halfmoves", C.c_uint16), ("fullmoves", C.c_uint16),
+                ("rep_key", C.c_uint64)]
+
+
+class AzNetDesc(C.Structure):
+    _fields_ = [("blocks", C.c_int), ("filters", C.c_int), ("dtype", C.c_int)]
+
+
+class AzSearchCfg(C.Structure):
+    _fields_ = [("games", C.c_int), ("sims", C.c_int), ("c_puct", C.c_float), ("dir_alpha", C.c_float),
+                ("dir_eps", C.c_float), ("temp_moves", C.c_int), ("noise", C.c_int), ("seed", C.c_uint64),
+                ("evaluator", C.c_int), ("continuous", C.c_int), ("record_evals", C.c_int),
+                ("eval_log_cap", C.c_int)]
+
+
+class AzEpisodeStep(C.Structure):
+    _fields_ = [("game_id", C.c_int32), ("ply", C.c_int32), ("action", C.c_int32), ("search_depth", C.c_int32),
+                ("final_value", C.c_float), ("result", C.c_int32), ("nvis", C.c_int32), ("state", AzPos),
+                ("vis_idx", C.c_uint16 * 224), ("vis_n", C.c_uint16 * 224)]
+
+
+class AzSearchStats(C.Structure):
+    _fields_ = [("sims", C.c_int64), ("evals", C.c_int64), ("terminal_leaves", C.c_int64),
+                ("games_finished", C.c_int64), ("moves", C.c_int64), ("max_depth_sum", C.c_int64)]
+
+
+class AzTiming(C.Structure):
+    _fields_ = [("conv_ms", C.c_double), ("conv_launches", C.c_int64), ("conv_flop", C.c_double),
+                ("tower_ms", C.c_double), ("tower_flop", C.c_double),
+                ("select_ms", C.c_double), ("select_launches", C.c_int64), ("select_bytes", C.c_double),
+                ("expand_ms", C.c_double), ("encode_ms", C.c_double), ("heads_ms", C.c_double),
+                ("backup_ms", C.c_double), ("sim_step_ms", C.c_double), ("sim_steps", C.c_int64),
+                ("rows", C.c_int64)]
+
+
+# every symbol include/az.h declares: (name, restype, argtypes)
+P = C.POINTER
+SIGNATURES = [
+    ("az_last_error", C.c_char_p, []),
+    ("az_version", C.c_int, []),
+    ("az_device_count", C.c_int, [P(C.c_int)]),
+    ("az_pos_startpos", C.c_int, [P(AzPos)]),
+    ("az_pos_from_fen", C.c_int, [C.c_char_p, P(AzPos)]),
+    ("az_pos_to_fen", C.c_int, [P(AzPos), C.c_char_p, C.c_int]),
+    ("az_pos_fen_key", C.c_uint64, [P(AzPos)]),
+    ("az_pos_legal_indices", C.c_int, [P(AzPos), P(C.c_int32), C.c_int]),
+    ("az_pos_play_index", C.c_int, [P(AzPos), C.c_int32, P(AzPos)]),
+    ("az_move_to_index", C.c_int, [C.c_int, C.c_int, C.c_int]),
+    ("az_pos_outcome", C.c_int, [P(AzPos)]),
+    ("az_pos_encode", C.c_int, [P(AzPos), P(C.c_float)]),
+    ("az_game_create", C.c_int, [P(C.c_void_p)]),
+    ("az_game_clone", C.c_int, [C.c_void_p, P(C.c_void_p)]),
+    ("az_game_destroy", C.c_int, [C.c_void_p]),
+    ("az_game_position", C.c_int, [C.c_void_p, P(AzPos)]),
+    ("az_game_history", C.c_int, [C.c_void_p, P(C.c_int32), C.c_int]),
+    ("az_game_play", C.c_int, [C.c_void_p, C.c_int32]),
+    ("az_net_num_params", C.c_size_t, [C.c_int, C.c_int]),
+    ("az_net_create", C.c_int, [P(AzNetDesc), P(C.c_float), C.c_size_t, C.c_int, P(C.c_void_p)]),
+    ("az_net_destroy", C.c_int, [C.c_void_p]),
+    ("az_net_forward", C.c_int, [C.c_void_p, P(C.c_float), C.c_int, P(C.c_float), P(C.c_float)]),
+    ("az_net_forward_device", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("az_search_default_cfg", C.c_int, [P(AzSearchCfg)]),
+    ("az_search_create", C.c_int, [C.c_void_p, P(AzSearchCfg), C.c_int, P(C.c_void_p)]),
+    ("az_search_destroy", C.c_int, [C.c_void_p]),
+    ("az_search_set_roots", C.c_int, [C.c_void_p, P(C.c_int32), P(C.c_int32), P(C.c_int32), P(C.c_int32),
+                                      C.c_int]),
+    ("az_search_run", C.c_int, [C.c_void_p, P(C.c_float), P(C.c_uint32), P(C.c_int32)]),
+    ("az_search_advance", C.c_int, [C.c_void_p, P(C.c_int32), C.c_int, P(C.c_int32)]),
+    ("az_selfplay_reset", C.c_int, [C.c_void_p]),
+    ("az_selfplay_step", C.c_int, [C.c_void_p, P(C.c_int), P(C.c_int)]),
+    ("az_selfplay_drain", C.c_int, [C.c_void_p, P(AzEpisodeStep), C.c_int]),
+    ("az_search_stats_get", C.c_int, [C.c_void_p, P(AzSearchStats)]),
+    ("az_search_eval_log", C.c_int, [C.c_void_p, P(C.c_int64), P(C.c_int64), P(C.c_uint64), P(C.c_float),
+                                     P(C.c_int32), P(C.c_int32), P(C.c_float)]),
+    ("az_search_timing", C.c_int, [C.c_void_p, P(AzTiming), C.c_int, C.c_int]),
+]
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError("libaz.so not built (%s); run __graft_entry__.build() or make -C %s" % (LIB_PATH, CSRC))
+
+lib = C.CDLL(LIB_PATH)
+for _name, _res, _args in SIGNATURES:
+    _f = getattr(lib, _name)
+    _f.restype = _res
+    _f.argtypes = _args
+
+
+class AzError(RuntimeError):
+    pass
+
+
+def check(rc):
+    if rc < 0:
+        raise AzError(lib.az_last_error().decode())
+    return rc
+
+
+def fptr(a):
+    return a.ctypes.data_as(P(C.c_float))
+
+
+def i32ptr(a):
+    return a.ctypes.data_as(P(C.c_int32))
+
+
+def u32ptr(a):
+    return a.ctypes.data_as(P(C.c_uint32))
+
+
+def u64ptr(a):
+    return a.ctypes.data_as(P(C.c_uint64))

@@ -1,0 +1,157 @@
+// az_internal.h -- shared definitions of libaz's translation units (not part of the ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+#include <vector>
+
+#include "../../include/az.h"
+#include "chess.h"
+
+static_assert(sizeof(az_pos) == 80, "az_pos layout");
+static_assert(sizeof(azc::Pos) == sizeof(az_pos), "Pos == az_pos");
+
+namespace azi {
+
+void set_error(const std::string& msg);
+int fail(const std::string& msg);
+
+#define AZ_HIP(expr)                                                                        \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess)                                                               \
+            return ::azi::fail(std::string(#expr) + ": " + hipGetErrorString(e_));          \
+    } while (0)
+
+// ---------------- search tree records (HBM, struct-of-arrays per game) ----------------
+struct Node {            // 16 B
+    uint32_t edge_begin; // first edge (game-relative)
+    uint16_t nedges;     // distinct legal move indices
+    uint16_t depth;      // root = 0
+    uint32_t nsum;       // sum of child visits (tree.rs:121 minus the +1)
+    int32_t parent;
+};
+struct Edge {            // 16 B, one dwordx4 per lane in the select walk
+    float P;             // prior (policy[i], noised at roots)
+    float W;             // scores[i]
+    uint16_t N;          // visits[i]
+    uint16_t idx;        // move index | PROMO_FLAG
+    int32_t child;       // node id, or CHILD_*
+};
+static_assert(sizeof(Node) == 16 && sizeof(Edge) == 16, "tree record layout");
+enum { CHILD_NONE = -1, CHILD_DRAW = -2, CHILD_WIN = -3 };
+enum { LEAF_EVAL = 0, LEAF_DRAW = 1, LEAF_WIN = 2 };
+constexpr int MAX_EDGES = 224;     // >= 218 legal moves
+constexpr int HMAX = 512;          // game history cap (200 fullmoves -> <= 400 plies)
+
+struct StepRec {                   // device -> host self-play record, 1024 B
+    int32_t game_id;
+    int16_t ply, action, depth, nvis, kind, result;   // kind 0 = step, 1 = game end
+    int16_t end_fullmoves, pad;
+    int32_t pad2;
+    azc::Pos pos;
+    uint16_t vis_idx[MAX_EDGES];
+    uint16_t vis_n[MAX_EDGES];
+    uint8_t tail[1024 - 24 - 80 - 4 * MAX_EDGES];
+};
+static_assert(sizeof(StepRec) == 1024, "StepRec");
+
+struct Counters {                  // device-side statistics
+    unsigned long long sims, evals, terminal, games_finished, moves, depth_sum, select_bytes;
+    int batch_count;
+    int rec_count;
+    int next_game_id;
+    int log_count;
+    int log_prior_count;
+    int overflow;
+    int pad[2];
+};
+
+// everything the tree kernels need, passed by value
+struct Engine {
+    int G, S, NMAX, EMAX, PMAX;
+    float c_puct, dir_alpha, dir_eps;
+    int temp_moves, noise, continuous;
+    unsigned long long seed;
+    Node* nodes;          // [G][NMAX]
+    azc::Pos* npos;       // [G][NMAX]
+    Edge* edges;          // [G][EMAX]
+    int* node_count; int* edge_count; int* max_depth;
+    int* leaf_node; int* leaf_edge; int* leaf_len; int* leaf_kind; int* leaf_row;
+    int* path_node; int* path_edge;        // [G][PMAX]
+    azc::Pos* hist; int* hist_len;         // [G][HMAX]
+    int* game_id; int* ply; int* active;
+    int* row_game; int* row_node;          // [G]
+    float* value;                          // [G] per batch row
+    const float* sqrt_tab;                 // [S + 2]
+    Edge* start_edges; int* start_n;       // startpos root template (priors un-noised)
+    StepRec* recs; int rec_cap;
+    Counters* ctr;
+    int* batch_hist;                       // [S] rows evaluated per sim step
+    // evaluation log
+    int log_cap, log_prior_cap;
+    unsigned long long* log_key; float* log_value; int* log_off; int* log_n; int* log_idx; float* log_prior;
+};
+
+// ---------------- network ----------------
+struct NetDev {
+    int blocks = 0, filters = 0, dtype = 0, device = 0;
+    std::vector<void*> conv_w;      // swizzled MFMA fragments per conv (1 + 2*blocks)
+    std::vector<float*> conv_b;     // folded bias per conv
+    float* head = nullptr;          // folded head weights (f32)
+    size_t head_floats = 0;
+    hipStream_t stream = nullptr;
+    // scratch for az_net_forward
+    void* x = nullptr; void* h = nullptr; void* planes = nullptr; int scratch_rows = 0;
+    float* d_in = nullptr; float* d_pol = nullptr; float* d_val = nullptr; int io_rows = 0;
+};
+
+// offsets inside NetDev::head
+struct HeadLayout {
+    size_t w40, b40, p2w, p2b, l1w, l1b, l2w, l2b, total;
+    __host__ __device__ static HeadLayout make(int F) {
+        HeadLayout L;
+        L.w40 = 0;                      // [40][F]: policy_conv_1 (32) then value_conv (8), BN folded
+        L.b40 = L.w40 + 40 * (size_t)F;
+        L.p2w = L.b40 + 40;             // [64][32]
+        L.p2b = L.p2w + 64 * 32;
+        L.l1w = L.p2b + 64;             // [512][64]
+        L.l1b = L.l1w + 512 * 64;
+        L.l2w = L.l1b + 64;             // [64]
+        L.l2b = L.l2w + 64;
+        L.total = L.l2b + 4;
+        return L;
+    }
+};
+
+// search-mode output target of the heads / synthetic evaluator
+struct SearchOut {
+    const Node* nodes; Edge* edges; int NMAX, EMAX;
+    const int* row_game; const int* row_node;
+    float* value;
+    // eval log (may be disabled: log_cap == 0)
+    int log_cap, log_prior_cap;
+    unsigned long long* log_key; float* log_value; int* log_off; int* log_n; int* log_idx; float* log_prior;
+    Counters* ctr;
+    const azc::Pos* npos;
+};
+
+int net_create(const az_net_desc* d, const float* w, size_t n, int device, NetDev** out);
+void net_destroy(NetDev* n);
+// planes [rows][64][32] in the net's dtype (device). count may be nullptr (all rows valid).
+// ev0/ev1 (optional) bracket the first residual conv launch (timing of one 3x3 FxF conv)
+int net_tower(NetDev* n, const void* planes, const int* count, int rows, void* x, void* h, hipStream_t st,
+              hipEvent_t ev0, hipEvent_t ev1);
+int net_heads_dense(NetDev* n, const void* x, int rows, float* policy, float* value, hipStream_t st);
+int net_heads_search(NetDev* n, const void* x, const int* count, int rows, const SearchOut& so, hipStream_t st);
+int net_encode_rows(NetDev* n, const azc::Pos* npos, int NMAX, const int* row_game, const int* row_node,
+                    const int* count, int rows, void* planes, hipStream_t st);
+int synth_eval_rows(const int* count, int rows, const SearchOut& so, hipStream_t st);
+int net_planes_from_host_layout(NetDev* n, const float* d_in, int rows, void* planes, hipStream_t st);
+size_t act_bytes(int dtype);
+double net_flop_per_eval(int blocks, int filters);
+double net_tower_flop_per_eval(int blocks, int filters);
+
+}  // namespace azi
+
+struct az_net { azi::NetDev* dev; };

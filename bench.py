@@ -1,0 +1,179 @@
+"""Benchmark: MCTS simulations/s of GPU-resident batched self-play (BASELINE.json metric).
+
+Workload (BASELINE.json configs[2], "C3"): 2048 concurrent self-play games per GPU,
+800 simulations per move, 20-block x 256-filter AlphaZero net (agent.rs), random-init
+weights (seed 42), all games from the start position (training.rs:344-358).
+One "step" = one move of every game = games x 800 simulations (select, expand, batched
+network evaluation, backup) + action choice / play / re-root.  Games that end are
+restarted in their slot, so every step does exactly games x sims simulations.
+Multi-GPU: one process per GPU, games sharded (different seeds), no collective on the
+path; barrier + max-over-ranks timing only.
+
+Extra JSON fields: roofline (the residual 3x3 conv kernel vs bf16 dense MFMA peak,
+measured with HIP events on the engine stream over the timed region), tree_walk (select
+kernel, algorithmic bytes / time vs HBM peak), cpu_baseline (the oracle, rank 0, N=1,
+bounded sample).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "alphazero-chess_amd"))
+
+PEAK_BF16_TFLOPS = 2500.0     # MI355X_MICROARCH.md: ~2.5 PF dense bf16
+PEAK_F32_TFLOPS = 157.3       # MI355X_MICROARCH.md: f32 MFMA = vector peak
+PEAK_HBM_GBS = 8000.0         # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def cpu_baseline(blocks, filters, threads, games, sims):
+    """Oracle (plain-C restatement of the reference, fp32) on the host cores: a bounded
+    sample of the same workload -- `games` searches of `sims` simulations each from the
+    start position with the same 20x256 net, one game per thread."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    import azchess as A
+    w = A.random_weights(blocks, filters, seed=42)
+    net = O.RefNet(blocks, filters, w)
+    cfg = O.make_cfg(sims=sims, noise=True, seed=42, eval_kind=1, net=net, threads=threads)
+    t0 = time.perf_counter()
+    steps, nsims, nevals = O.selfplay(cfg, games, max_plies=1)
+    dt = time.perf_counter() - t0
+    return {"value": nsims / dt, "unit": "sims/s", "cores": threads, "kind": "port",
+            "sample": "%d games x 1 move x %d sims (+ shared root eval), %dx%d fp32 oracle, %d threads, %.1f s"
+                      % (games, sims, blocks, filters, threads, dt),
+            "evals": nevals}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--games", type=int, default=2048)
+    ap.add_argument("--sims", type=int, default=800)
+    ap.add_argument("--blocks", type=int, default=20)
+    ap.add_argument("--filters", type=int, default=256)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-games", type=int, default=16)
+    ap.add_argument("--cpu-sims", type=int, default=8)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    import azchess as A
+
+    G, S = args.games, args.sims
+    net = A.AlphaZero(args.blocks, args.filters, dtype=args.dtype, device=local, seed=42)
+    sp = A.SelfPlay(net, games=G, sims=S, device=local, continuous=True, seed=42 + 1000003 * rank)
+    sp.reset()
+    for _ in range(args.warmup):
+        sp.step()
+        sp.drain()
+    st0 = sp.search.stats()
+    sp.search.timing(reset=True, enable=True)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    finished = 0
+    for _ in range(args.steps):
+        f, _ = sp.step()
+        finished += f
+        sp.drain()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    tm = sp.search.timing(reset=False, enable=False)
+    st1 = sp.search.stats()
+    sims_rank = st1["sims"] - st0["sims"]
+    evals_rank = st1["evals"] - st0["evals"]
+    term_rank = st1["terminal_leaves"] - st0["terminal_leaves"]
+    moves_rank = st1["moves"] - st0["moves"]
+    depth_rank = st1["max_depth_sum"] - st0["max_depth_sum"]
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        c = torch.tensor([sims_rank, evals_rank, term_rank, finished, moves_rank, depth_rank], dtype=torch.float64,
+                         device="cuda")
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        sims_all, evals_all, term_all, fin_all, moves_all, depth_all = [float(v) for v in c.tolist()]
+    else:
+        sims_all, evals_all, term_all, fin_all, moves_all, depth_all = (sims_rank, evals_rank, term_rank, finished,
+                                                                        moves_rank, depth_rank)
+    assert sims_rank == G * S * args.steps, (sims_rank, G * S * args.steps)
+
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+    value = sims_all / elapsed
+    peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
+    conv_tflops = tm["conv_flop"] / (tm["conv_ms"] * 1e-3) / 1e12 if tm["conv_ms"] > 0 else 0.0
+    tower_tflops = tm["tower_flop"] / (tm["tower_ms"] * 1e-3) / 1e12 if tm["tower_ms"] > 0 else 0.0
+    sel_gbs = tm["select_bytes"] / (tm["select_ms"] * 1e-3) / 1e9 if tm["select_ms"] > 0 else 0.0
+    out = {
+        "metric": "MCTS sims/sec at 800 sims/move, 20x256 net; self-play games/hr at 1/2/4/8 GPU",
+        "value": value,
+        "unit": "sims/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic: random-init %dx%d weights (seed 42), self-play from startpos, Dirichlet noise on"
+                % (args.blocks, args.filters),
+        "config": {"workload": "C3 (BASELINE.json configs[2]): %d concurrent self-play games/GPU x %d sims/move, "
+                               "%d-block x %d-filter net" % (G, S, args.blocks, args.filters),
+                   "games_per_gpu": G, "sims_per_move": S, "blocks": args.blocks, "filters": args.filters,
+                   "parallelism": "games sharded %d-way, no collective" % world},
+        "roofline": {"bound": "mfma", "achieved": conv_tflops, "peak": peak, "unit": "TFLOP/s",
+                     "frac": conv_tflops / peak, "traffic": None,
+                     "kernel": "conv3x3_kernel<%d,%d> (residual 3x3 conv), %d launches timed" %
+                               (args.filters, args.filters, tm["conv_launches"]),
+                     "flop_per_launch": tm["conv_flop"] / max(tm["conv_launches"], 1),
+                     "avg_ms_per_launch": tm["conv_ms"] / max(tm["conv_launches"], 1)},
+        "tower": {"achieved_tflops": tower_tflops, "frac": tower_tflops / peak,
+                  "ms_per_sim_step": tm["tower_ms"] / max(tm["sim_steps"], 1)},
+        "tree_walk": {"kernel": "k_select", "achieved_gbs": sel_gbs, "peak_gbs": PEAK_HBM_GBS,
+                      "frac": sel_gbs / PEAK_HBM_GBS,
+                      "bytes_per_sim": tm["select_bytes"] / max(sims_rank, 1),
+                      "avg_ms_per_launch": tm["select_ms"] / max(tm["select_launches"], 1)},
+        "sim_step_ms": {k: tm[k + "_ms"] / max(tm["sim_steps"], 1)
+                        for k in ("select", "expand", "encode", "tower", "heads", "backup")},
+        "evals_per_sim": evals_all / max(sims_all, 1),
+        "terminal_leaf_frac": term_all / max(sims_all, 1),
+        "avg_search_depth": depth_all / max(moves_all, 1),
+        "games_finished": int(fin_all),
+        "games_per_hr": fin_all / elapsed * 3600.0,
+        "cpu_baseline": None,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.blocks, args.filters, args.cpu_threads, args.cpu_games,
+                                           args.cpu_sims)
+    print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,182 @@
+/*
+ * az.h -- C-ABI of the MI355X-native alphazero-chess self-play engine (libaz.so).
+ *
+ * Drop-in boundary for the reference's hot path (AlexandreGac/alphazero-chess @ 2025-08-24).
+ * The reference is a single Rust crate with no FFI; each entry point below replaces one
+ * item of its module surface (file:line cited) and is what a Rust `extern "C"` block
+ * would bind (see INTEGRATION.md for the binding a maintainer would add).
+ *
+ * Conventions: every function returns int status (0 = ok, <0 = error; message via
+ * az_last_error()) unless noted.  Plain pointers and sizes only.  Host buffers are
+ * caller-owned; the engine owns all device memory.  A handle is used by one host thread
+ * at a time (not re-entrant); one handle per GPU.
+ * Squares: a1 = 0 ... h8 = 63 (shakmaty Square order).  Move indices: 0..4095 =
+ * plane*64 + rank'*8 + file (chess.rs:73-116), rank' flipped for Black.
+ */
+#ifndef AZ_H
+#define AZ_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AZ_ACTION_SPACE 4096   /* parameters.rs:3 */
+#define AZ_PLANES 19           /* chess.rs:191-245 */
+#define AZ_MAX_MOVES 256
+
+/* Result codes of play (chess.rs:29-34 GameResult, plus -1 = Err("Illegal move")) */
+enum { AZ_ONGOING = 0, AZ_DRAW = 1, AZ_WHITE_WINS = 2, AZ_BLACK_WINS = 3, AZ_ILLEGAL = -1 };
+
+/* Packed position (80 bytes) -- the engine's replacement for shakmaty::Chess.
+ * bb: P N B R Q K (both colours), white, black.  ep: pseudo-legal en-passant square
+ * (shakmaty pseudo_legal_ep_square, chess.rs:218) or 64.  flags bit0: that ep capture is
+ * also legal (shakmaty Chess equality uses the legal ep square).  castling bits:
+ * 1 = White O-O, 2 = White O-O-O, 4 = Black O-O, 8 = Black O-O-O.
+ * rep_key: hash of (board, turn, castling, legal ep) -- the repetition key. */
+typedef struct az_pos {
+    uint64_t bb[8];
+    uint8_t turn, castling, ep, flags;
+    uint16_t halfmoves, fullmoves;
+    uint64_t rep_key;
+} az_pos;
+
+const char* az_last_error(void);
+int az_version(void);
+int az_device_count(int* n);
+
+/* ---- rules & codec: chess.rs ---------------------------------------------------- */
+int az_pos_startpos(az_pos* out);                                   /* Chess::new, chess.rs:21 */
+int az_pos_from_fen(const char* fen, az_pos* out);
+int az_pos_to_fen(const az_pos* p, char* buf, int cap);            /* Fen::from_position(.., PseudoLegal) */
+uint64_t az_pos_fen_key(const az_pos* p);                           /* cache key, tree.rs:214 */
+/* legal move indices in shakmaty legal_moves() order WITH duplicates for
+ * under-promotions, exactly MCTree::new's `moves` (tree.rs:86-89). Returns count. */
+int az_pos_legal_indices(const az_pos* p, int32_t* out, int cap);
+/* index_to_move (chess.rs:118-171) + play_unchecked: returns 1 and writes the child
+ * position if the index names a legal move, 0 otherwise. */
+int az_pos_play_index(const az_pos* p, int32_t index, az_pos* child);
+int az_move_to_index(int from, int to, int turn);                   /* chess.rs:73-116 */
+/* outcome(): AZ_ONGOING, AZ_DRAW (stalemate / insufficient material), AZ_WHITE/BLACK_WINS */
+int az_pos_outcome(const az_pos* p);
+int az_pos_encode(const az_pos* p, float* out);                     /* to_tensor, chess.rs:191-245: 19*64 f32 */
+
+/* GameState = position + repetition multiset (chess.rs:13-27) */
+typedef struct az_game az_game;
+int az_game_create(az_game** out);                                  /* GameState::new, chess.rs:20 */
+int az_game_clone(const az_game* g, az_game** out);
+int az_game_destroy(az_game* g);
+int az_game_position(const az_game* g, az_pos* out);
+int az_game_history(const az_game* g, int32_t* moves, int cap);     /* indices played so far; returns count */
+/* play_move(state, index_to_move(index)) (chess.rs:36-63): AZ_ONGOING / AZ_DRAW /
+ * AZ_WHITE_WINS / AZ_BLACK_WINS / AZ_ILLEGAL */
+int az_game_play(az_game* g, int32_t index);
+
+/* ---- network: agent.rs AlphaZero ------------------------------------------------- */
+enum { AZ_DTYPE_F32 = 0, AZ_DTYPE_BF16 = 1 };
+typedef struct { int blocks, filters, dtype; } az_net_desc;
+typedef struct az_net az_net;
+/* number of f32 parameters in the flat layout (see DESIGN.md "Weights"): burn module
+ * order, conv [out,in,kh,kw], BatchNorm {gamma,beta,running_mean,running_var},
+ * Linear weight [d_in,d_out] (burn layout). */
+size_t az_net_num_params(int blocks, int filters);
+/* AlphaZero::new + load_record (agent.rs:49-110, main.rs:109-116): weights copied to HBM,
+ * BatchNorm folded into the convs (inference mode, model.valid()). */
+int az_net_create(const az_net_desc* desc, const float* weights, size_t n, int device, az_net** out);
+int az_net_destroy(az_net* net);
+/* AlphaZero::forward (agent.rs:112-144): planes [n,19,8,8] f32 -> policy [n,4096]
+ * (softmax) and value [n] (tanh). Host buffers. */
+int az_net_forward(az_net* net, const float* planes, int n, float* policy, float* value);
+/* Same on device pointers / a caller's hipStream_t (NULL = engine stream). */
+int az_net_forward_device(az_net* net, const float* d_planes, int n, float* d_policy, float* d_value,
+                          void* stream);
+
+/* ---- search: tree.rs MCTree + training.rs self-play driver ------------------------ */
+enum { AZ_EVAL_NET = 0, AZ_EVAL_SYNTHETIC = 1 };
+typedef struct {
+    int games;          /* concurrent games G on this GPU (NUM_EPISODES, parameters.rs:13) */
+    int sims;           /* simulations per move (NUM_SIMULATIONS, parameters.rs:32) */
+    float c_puct;       /* parameters.rs:34 */
+    float dir_alpha;    /* parameters.rs:28 */
+    float dir_eps;      /* parameters.rs:29 */
+    int temp_moves;     /* TEMPERATURE_ANNEALING, parameters.rs:31 */
+    int noise;          /* Dirichlet noise at roots (training.rs:358, tree.rs:243) */
+    uint64_t seed;      /* counter-based RNG seed (replaces thread_rng) */
+    int evaluator;      /* AZ_EVAL_NET or AZ_EVAL_SYNTHETIC */
+    int continuous;     /* self-play: restart a finished slot with a new game */
+    int record_evals;   /* keep a log of every evaluation (for replay parity) */
+    int eval_log_cap;   /* log capacity in rows */
+} az_search_cfg;
+typedef struct az_search az_search;
+
+int az_search_default_cfg(az_search_cfg* cfg);   /* reference defaults (parameters.rs) */
+int az_search_create(az_net* net, const az_search_cfg* cfg, int device, az_search** out);
+int az_search_destroy(az_search* s);
+
+/* Roots from histories: game g's root = startpos + hist[off[g]..off[g+1]) (move indices),
+ * evaluated and optionally noised: MCTree::new(policy, state, apply_noise), tree.rs:84-104.
+ * noise_ply[g] (may be NULL = 0) selects the RNG stream (seed, game_id[g], ply). */
+int az_search_set_roots(az_search* s, const int32_t* hist, const int32_t* off, const int32_t* game_id,
+                        const int32_t* noise_ply, int apply_noise);
+/* monte_carlo_tree_search for every game (tree.rs:106-115 / 169-178).  Outputs (any may
+ * be NULL): improved policy [G,4096], visits [G,4096], max_subtree_depth [G]. */
+int az_search_run(az_search* s, float* improved, uint32_t* visits, int32_t* depth);
+/* traverse_new(action, apply_noise) for every game (tree.rs:239-256) after playing the
+ * action on its GameState (training.rs:323-325).  result[g] receives the play_move result. */
+int az_search_advance(az_search* s, const int32_t* actions, int apply_noise, int32_t* result);
+
+/* run_all_episodes (training.rs:340-378): reset all G slots to new games from startpos */
+int az_selfplay_reset(az_search* s);
+/* one move for every active game: sims, improved policy, action choice (training.rs:310-321),
+ * play, traverse/record.  *finished = games that ended in this step. */
+int az_selfplay_step(az_search* s, int* finished, int* active);
+
+/* EpisodeStep (training.rs:15-20) of finished games, drained in game order. */
+typedef struct {
+    int32_t game_id;
+    int32_t ply;
+    int32_t action;
+    int32_t search_depth;
+    float final_value;         /* training.rs:332-335 */
+    int32_t result;            /* AZ_DRAW / AZ_WHITE_WINS / AZ_BLACK_WINS */
+    int32_t nvis;              /* improved_policy = visits / sum(visits) over these entries */
+    az_pos state;
+    uint16_t vis_idx[224];
+    uint16_t vis_n[224];
+} az_episode_step;
+int az_selfplay_drain(az_search* s, az_episode_step* out, int cap);   /* returns count */
+
+typedef struct {
+    int64_t sims;              /* simulations completed */
+    int64_t evals;             /* network rows evaluated */
+    int64_t terminal_leaves;
+    int64_t games_finished;
+    int64_t moves;
+    int64_t max_depth_sum;     /* sum over moves of max_subtree_depth */
+} az_search_stats;
+int az_search_stats_get(az_search* s, az_search_stats* out);
+
+/* Evaluation log (cfg.record_evals): keys[n] (fen keys), values[n], CSR priors at the
+ * legal move indices. Pass NULL arrays to query sizes. */
+int az_search_eval_log(az_search* s, int64_t* n_rows, int64_t* n_priors, uint64_t* keys, float* values,
+                       int32_t* off, int32_t* idx, float* priors);
+
+/* Profiling: device times measured with HIP events on the engine stream while enabled.
+ * conv_*: the first residual 3x3 FxF conv of every simulation step (the dominant kernel);
+ * conv_flop = algorithmic FLOPs of those launches (rows * 2*64*9*F*F).  tower_*: the whole
+ * conv tower.  select_bytes: algorithmic bytes read by the select walk (16 B per edge +
+ * 16 B node + 4 B sqrt per level). */
+typedef struct {
+    double conv_ms;      int64_t conv_launches;  double conv_flop;
+    double tower_ms;     double tower_flop;
+    double select_ms;    int64_t select_launches; double select_bytes;
+    double expand_ms;    double encode_ms;       double heads_ms;    double backup_ms;
+    double sim_step_ms;  int64_t sim_steps;      int64_t rows;
+} az_timing;
+int az_search_timing(az_search* s, az_timing* out, int reset, int enable);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,80 @@
+"""HIP network (MFMA conv tower + fused heads) against the torch golden vectors and the
+oracle.  Tolerances (stated per north_star "policy/value within a stated fp tolerance"):
+  f32 path (v_mfma_f32_16x16x4_f32, exact f32 FMA chains, BN folded):
+      value |d| <= 1e-5, policy |d| <= 1e-4 * p + 1e-8
+  bf16 path (bf16 weights/activations, f32 accumulate):
+      value |d| <= 2e-2, policy |d| <= 5e-2 * p + 2e-5 and total-variation <= 2e-2
+"""
+import os
+
+import numpy as np
+import pytest
+
+import azchess as A
+import oracle as O
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+TOL = {"f32": dict(v=1e-5, prel=1e-4, pabs=1e-8), "bf16": dict(v=2e-2, prel=5e-2, pabs=2e-5)}
+
+
+def golden():
+    return np.load(os.path.join(ROOT, "tests", "golden", "net_2x32.npz"))
+
+
+def check(pol, val, rpol, rval, dtype):
+    t = TOL[dtype]
+    assert np.all(np.abs(val - rval) <= t["v"]), np.abs(val - rval).max()
+    err = np.abs(pol - rpol) - (t["prel"] * rpol + t["pabs"])
+    assert np.all(err <= 0), (np.abs(pol - rpol) / (rpol + 1e-12)).max()
+    if dtype == "bf16":
+        assert np.max(0.5 * np.abs(pol - rpol).sum(1)) <= 2e-2
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_net_matches_torch_golden(require_gpu, dtype):
+    g = golden()
+    net = A.AlphaZero(int(g["blocks"]), int(g["filters"]), weights=g["weights"], dtype=dtype)
+    pol, val = net.forward(g["planes"])
+    check(pol, val, g["policy"].astype(np.float64), g["value"].astype(np.float64), dtype)
+
+
+def random_planes(n, seed):
+    rng = np.random.default_rng(seed)
+    out = []
+    while len(out) < n:
+        gs = A.GameState()
+        for _ in range(int(rng.integers(0, 60))):
+            idx = gs.position.legal_indices()
+            if len(idx) == 0 or int(A.play_move(gs, int(rng.choice(idx)))) != 0:
+                break
+        if len(gs.position.legal_indices()):
+            out.append(A.to_tensor(gs.position)[0])
+    return np.stack(out)
+
+
+@pytest.mark.parametrize("blocks,filters,dtype,n", [(6, 64, "f32", 24), (6, 64, "bf16", 24), (2, 128, "bf16", 9),
+                                                    (20, 256, "bf16", 6), (20, 256, "f32", 6)])
+def test_net_matches_oracle(require_gpu, blocks, filters, dtype, n):
+    w = A.random_weights(blocks, filters, seed=42)
+    planes = random_planes(n, blocks * 1000 + filters)
+    net = A.AlphaZero(blocks, filters, weights=w, dtype=dtype)
+    pol, val = net.forward(planes)
+    ref = O.RefNet(blocks, filters, w)
+    rpol, rval = ref.forward(planes, threads=16)
+    check(pol, val, rpol.astype(np.float64), rval.astype(np.float64), dtype)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_rows_are_batch_independent(require_gpu, dtype):
+    """Every row is computed independently of the batch it sits in (needed for replay parity
+    and for the FEN-cache equivalence, tree.rs:214)."""
+    planes = random_planes(13, 5)
+    net = A.AlphaZero(2, 64, dtype=dtype)
+    pol, val = net.forward(planes)
+    for i in (0, 5, 12):
+        p1, v1 = net.forward(planes[i:i + 1])
+        assert np.array_equal(p1[0], pol[i]) and v1[0] == val[i]
+    p2, v2 = net.forward(np.concatenate([planes[7:], planes[:7]]))
+    assert np.array_equal(p2[:6], pol[7:]) and np.array_equal(v2[6:], val[:7])

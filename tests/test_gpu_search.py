@@ -1,0 +1,125 @@
+"""GPU search (select/expand/backup kernels, noise, move choice) against the oracle's
+restatement of tree.rs / training.rs.  Bar: BIT-EXACT visit counts, chosen actions, search
+depths and final values -- with the synthetic evaluator (identical definition on both
+sides) and with the network's own evaluations replayed into the oracle."""
+import numpy as np
+import pytest
+
+import azchess as A
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def histories(n, seed, max_len=30):
+    rng = np.random.default_rng(seed)
+    out = []
+    while len(out) < n:
+        gs, h = A.GameState(), []
+        for _ in range(int(rng.integers(0, max_len))):
+            idx = gs.position.legal_indices()
+            a = int(rng.choice(idx))
+            if int(A.play_move(gs, a)) != 0:
+                break
+            h.append(a)
+        else:
+            pass
+        if int(gs.position.outcome()) == 0 and len(gs.position.legal_indices()):
+            # only roots whose history did not already end the game
+            ok = True
+            g2 = A.GameState()
+            for a in h:
+                ok &= int(A.play_move(g2, a)) == 0
+            if ok:
+                out.append(h)
+    return out
+
+
+@pytest.mark.parametrize("noise", [False, True])
+@pytest.mark.parametrize("sims", [16, 100])
+def test_search_synthetic_bit_exact(require_gpu, noise, sims):
+    hs = histories(12, sims + noise)
+    s = A.BatchedSearch(None, games=len(hs), sims=sims, noise=noise, seed=11)
+    s.set_roots(hs, apply_noise=noise)
+    imp, vis, dep = s.run()
+    cfg = O.make_cfg(sims=sims, noise=noise, seed=11, eval_kind=0)
+    for g, h in enumerate(hs):
+        key = O.lib().ref_stream_key(11, g, len(h), 0)
+        rv, ri, rd, _ = O.search_game(cfg, h, noise=noise, noise_key=key)
+        assert np.array_equal(vis[g].astype(np.float32), rv), g
+        assert np.array_equal(imp[g], ri), g
+        assert dep[g] == rd
+
+
+def compare_steps(gpu_steps, ref_steps):
+    gs = sorted(gpu_steps, key=lambda s: (s.game_id, s.ply))
+    rs = sorted(ref_steps, key=lambda s: (s["game"], s["ply"]))
+    assert len(gs) == len(rs)
+    for a, b in zip(gs, rs):
+        assert (a.game_id, a.ply, a.action, a.search_depth, a.result) == \
+               (b["game"], b["ply"], b["action"], b["depth"], b["result"]), (a.game_id, a.ply)
+        assert a.visits == {k: int(v) for k, v in b["visits"].items()}
+        assert np.float32(a.final_value) == np.float32(b["final_value"])
+
+
+def test_selfplay_synthetic_bit_exact(require_gpu):
+    games, sims = 6, 16
+    avg, steps = A.run_all_episodes(None, games=games, sims=sims, seed=5)
+    ref, rsims, _ = O.selfplay(O.make_cfg(sims=sims, noise=True, seed=5, eval_kind=0), games)
+    compare_steps(steps, ref)
+    assert {s.game_id for s in steps} == set(range(games))
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
+def test_selfplay_net_replay_bit_exact(require_gpu, dtype):
+    """Self-play with the 2x32 network; the oracle replays the GPU's evaluations and must
+    reproduce every visit count / action / depth / final value.  The evaluations
+    themselves are checked against the oracle network within the dtype tolerance."""
+    games, sims = 4, 16
+    w = A.random_weights(2, 32, seed=42)
+    net = A.AlphaZero(2, 32, weights=w, dtype=dtype)
+    sp = A.SelfPlay(net, games=games, sims=sims, seed=9, record_evals=True, eval_log_cap=1 << 17)
+    sp.reset()
+    steps = []
+    for _ in range(600):
+        _, active = sp.step()
+        steps += sp.drain()
+        if active == 0:
+            break
+    keys, vals, off, idx, pri = sp.search.eval_log()
+    rep = O.Replay(keys, vals, off, idx, pri)
+    ref, _, _ = O.selfplay(O.make_cfg(sims=sims, noise=True, seed=9, eval_kind=2), games, replay=rep)
+    compare_steps(steps, ref)
+    # evaluations vs the oracle network (first 64 logged rows)
+    ref_net = O.RefNet(2, 32, w)
+    pos_by_key = {}
+    for s in steps:
+        pos_by_key.setdefault(s.state.fen_key(), s.state)
+    tol = {"bf16": (2e-2, 5e-2, 2e-5), "f32": (1e-5, 1e-4, 1e-8)}[dtype]
+    checked = 0
+    for r in range(len(keys)):
+        p = pos_by_key.get(int(keys[r]))
+        if p is None:
+            continue
+        rpol, rval = ref_net.forward(A.to_tensor(p))
+        assert abs(vals[r] - rval[0]) <= tol[0]
+        ii = idx[off[r]:off[r + 1]]
+        assert np.all(np.abs(pri[off[r]:off[r + 1]] - rpol[0][ii]) <= tol[1] * rpol[0][ii] + tol[2])
+        checked += 1
+        if checked >= 64:
+            break
+    assert checked > 10
+
+
+def test_large_batch_invariants(require_gpu):
+    """C3-sized batch (2048 games, 20x256 bf16) for a few simulations: size-independent
+    properties -- root visit sums equal the simulations run, priors are distributions."""
+    net = A.AlphaZero(20, 256, dtype="bf16")
+    G, S = 2048, 4
+    s = A.BatchedSearch(net, games=G, sims=S, seed=1)
+    s.set_roots([[]] * G, apply_noise=True)
+    imp, vis, dep = s.run()
+    assert np.all(vis.sum(1) == S)
+    assert np.allclose(imp.sum(1), 1.0, atol=1e-6)
+    st = s.stats()
+    assert st["sims"] == G * S and st["evals"] == st["sims"] - st["terminal_leaves"]

@@ -1,0 +1,77 @@
+"""Product rules/codec (libaz host entry points, the same chess.h the GPU runs) against
+the oracle on random playouts and edge positions: legal index lists (order and
+duplicates), play_move results incl. repetition / 50-move / 200-fullmove, to_tensor,
+FEN and the FEN key.  CPU only (no device calls)."""
+import numpy as np
+import pytest
+
+import azchess as A
+import oracle as O
+
+EDGE_FENS = [
+    "r3k2r/p1ppqpb1/bn2pnp1/3PN3/1p2P3/2N2Q1p/PPPBBPPP/R3K2R w KQkq - 0 1",
+    "8/2p5/3p4/KP5r/1R3p1k/8/4P1P1/8 w - - 0 1",
+    "r3k2r/Pppp1ppp/1b3nbN/nP6/BBP1P3/q4N2/Pp1P2PP/R2Q1RK1 w kq - 0 1",
+    "rnbq1k1r/pp1Pbppp/2p5/8/2B5/8/PPP1NnPP/RNBQK2R w KQ - 1 8",
+    "8/8/8/2k5/3Pp3/8/8/4K3 b - d3 0 1",          # ep available
+    "8/8/8/8/k2Pp2Q/8/8/3K4 b - d3 0 1",          # ep illegal (horizontal pin)
+    "8/8/8/1k6/3Pp3/8/8/4KQ2 b - d3 0 1",
+    "4k3/8/8/8/8/8/8/R3K2R w KQ - 0 1",
+    "r3k2r/8/8/8/8/8/8/R3K2R b KQkq - 0 1",
+    "r3k2r/8/8/8/8/5q2/8/R3K2R w KQkq - 0 1",      # castling through check
+    "4k3/1P6/8/8/8/8/6p1/4K3 w - - 0 1",          # promotions both sides
+    "3k4/8/8/8/8/8/8/3KQ3 b - - 99 150",
+    "7k/6Q1/6K1/8/8/8/8/8 b - - 0 1",             # checkmate
+    "7k/5Q2/6K1/8/8/8/8/8 b - - 0 1",             # stalemate
+]
+
+
+def same_position(pa, po):
+    assert pa.fen() == O.to_fen(po)
+    assert list(pa.legal_indices()) == list(O.legal_indices(po))
+    assert np.array_equal(A.to_tensor(pa)[0], O.to_tensor(po))
+    assert pa.fen_key() == O.fen_key(po)
+    assert np.array_equal(pa.bitboards(), O.bitboards(po))
+    assert int(pa.outcome()) == O.outcome(po)
+
+
+@pytest.mark.parametrize("fen", EDGE_FENS)
+def test_edge_positions(fen):
+    same_position(A.Position.from_fen(fen), O.from_fen(fen))
+
+
+def test_random_playouts_match_oracle():
+    rng = np.random.default_rng(7)
+    for game in range(60):
+        ga, go = A.GameState(), O.Game()
+        for ply in range(400):
+            pa, po = ga.position, go.position
+            same_position(pa, po)
+            idx = pa.legal_indices()
+            if len(idx) == 0:
+                break
+            a = int(rng.choice(idx))
+            assert A.index_to_move(a, pa) == a
+            ra = int(A.play_move(ga, a))
+            ro = go.play_index(a)
+            assert ra == ro, (game, ply, pa.fen(), a)
+            if ra != 0:
+                break
+
+
+def test_repetition_draw_matches():
+    ga, go = A.GameState(), O.Game()
+    seq = []
+    for _ in range(2):
+        seq += [A.move_to_index(6, 21, 0), A.move_to_index(62, 45, 1), A.move_to_index(21, 6, 0),
+                A.move_to_index(45, 62, 1)]
+    for i, a in enumerate(seq):
+        ra, ro = int(A.play_move(ga, a)), go.play_index(a)
+        assert ra == ro == (1 if i == len(seq) - 1 else 0)
+
+
+def test_illegal_index_rejected():
+    p = A.Position.startpos()
+    assert A.index_to_move(0, p) is None        # a1 has a rook that cannot jump
+    with pytest.raises(A.IllegalMove):
+        A.play_move(A.GameState(), 0)
