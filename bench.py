@@ -63,9 +63,8 @@ def main():
     ap.add_argument("--cpu-sims", type=int, default=8)
     args = ap.parse_args()
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from azchess.dist import barrier as dist_barrier, env_rank, reduce_run, shard
+    rank, world, local = env_rank()
     import torch
     import torch.distributed as dist
     if world > 1:
@@ -77,7 +76,8 @@ def main():
 
     G, S = args.games, args.sims
     net = A.AlphaZero(args.blocks, args.filters, dtype=args.dtype, device=local, seed=42)
-    sp = A.SelfPlay(net, games=G, sims=S, device=local, continuous=True, seed=42 + 1000003 * rank)
+    sh = shard(rank, world, G)
+    sp = A.SelfPlay(net, games=G, sims=S, device=local, continuous=True, seed=sh["seed"])
     sp.reset()
     for _ in range(args.warmup):
         sp.step()
@@ -86,8 +86,7 @@ def main():
     sp.search.timing(reset=True, enable=True)
 
     def barrier():
-        if world > 1:
-            dist.barrier()
+        dist_barrier(world)
         torch.cuda.synchronize()
 
     barrier()
@@ -107,17 +106,9 @@ def main():
     term_rank = st1["terminal_leaves"] - st0["terminal_leaves"]
     moves_rank = st1["moves"] - st0["moves"]
     depth_rank = st1["max_depth_sum"] - st0["max_depth_sum"]
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        c = torch.tensor([sims_rank, evals_rank, term_rank, finished, moves_rank, depth_rank], dtype=torch.float64,
-                         device="cuda")
-        dist.all_reduce(c, op=dist.ReduceOp.SUM)
-        sims_all, evals_all, term_all, fin_all, moves_all, depth_all = [float(v) for v in c.tolist()]
-    else:
-        sims_all, evals_all, term_all, fin_all, moves_all, depth_all = (sims_rank, evals_rank, term_rank, finished,
-                                                                        moves_rank, depth_rank)
+    elapsed, tot = reduce_run(elapsed, [sims_rank, evals_rank, term_rank, finished, moves_rank, depth_rank], world,
+                              device="cuda")
+    sims_all, evals_all, term_all, fin_all, moves_all, depth_all = tot
     assert sims_rank == G * S * args.steps, (sims_rank, G * S * args.steps)
 
     if rank != 0:
