@@ -60,6 +60,7 @@ SIGNATURES = [
     ("az_last_error", C.c_char_p, []),
     ("az_version", C.c_int, []),
     ("az_device_count", C.c_int, [P(C.c_int)]),
+    ("az_device_synchronize", C.c_int, [C.c_int]),
     ("az_pos_startpos", C.c_int, [P(AzPos)]),
     ("az_pos_from_fen", C.c_int, [C.c_char_p, P(AzPos)]),
     ("az_pos_to_fen", C.c_int, [P(AzPos), C.c_char_p, C.c_int]),
@@ -100,6 +101,21 @@ if not os.path.exists(LIB_PATH):
     raise ImportError("libaz.so not built (%s); run __graft_entry__.build() or make -C %s" % (LIB_PATH, CSRC))
 
 lib = C.CDLL(LIB_PATH)
+
+
+def hip_runtime_paths():
+    """HIP runtime(s) mapped in this process (libaz is built for /opt/rocm's; torch bundles
+    another libamdhip64.so.7 with the same SONAME, so import azchess BEFORE torch)."""
+    try:
+        return sorted({l.split()[-1] for l in open("/proc/self/maps") if "libamdhip64" in l})
+    except OSError:
+        return []
+
+
+_rt = hip_runtime_paths()
+if _rt and not any(p.startswith("/opt/rocm") for p in _rt):
+    import warnings
+    warnings.warn("libaz bound to a non-/opt/rocm HIP runtime %s (torch imported first?)" % _rt)
 for _name, _res, _args in SIGNATURES:
     _f = getattr(lib, _name)
     _f.restype = _res

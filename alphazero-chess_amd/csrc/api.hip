@@ -47,6 +47,12 @@ int az_device_count(int* n) {
     return 0;
 }
 
+int az_device_synchronize(int device) {
+    AZ_HIP(hipSetDevice(device));
+    AZ_HIP(hipDeviceSynchronize());
+    return 0;
+}
+
 int az_pos_startpos(az_pos* out) {
     if (!out) return fail("null");
     P(out) = azc::startpos();

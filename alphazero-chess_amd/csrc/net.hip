@@ -55,12 +55,14 @@ conv3x3_kernel(const T* __restrict__ in, T* __restrict__ out, const void* __rest
     constexpr int NT = COUT * 2;                      // COUT/32 waves
     constexpr int CHS = DTraits<T>::CH_SLOT;          // channels per 16-B slot
     constexpr int NSLOT = CIN / CHS;
-    constexpr int SWZ = (NSLOT - 1) < 15 ? (NSLOT - 1) : 15;
+    constexpr int RS = NSLOT + 2;                     // padded row stride (slots): conflict-free ds_read_b128
     constexpr int CHUNK = DTraits<T>::CHUNK;          // channels per K-chunk (4 slots)
     constexpr int NCH = CIN / CHUNK;
     constexpr int CF = COUT / 16;
     constexpr int MF = BPB * 4;                       // 16-square fragments per block
-    __shared__ __attribute__((aligned(16))) uint4 lds[(BPB * 64 + 1) * NSLOT];
+    constexpr int ZB = BPB * 64 * RS;                 // zero region (read by off-board taps)
+    constexpr int ZN = 16 + NSLOT;
+    __shared__ __attribute__((aligned(16))) uint4 lds[ZB + ZN];
 
     const int count = count_ptr ? min(*count_ptr, rows) : rows;
     const int row0 = blockIdx.x * BPB;
@@ -69,50 +71,52 @@ conv3x3_kernel(const T* __restrict__ in, T* __restrict__ out, const void* __rest
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
 
-    // stage the boards (zero-fill missing boards and the zero row)
+    // stage the boards into padded rows (missing boards and the zero region are zero)
     const uint4* src = reinterpret_cast<const uint4*>(in) + (size_t)row0 * 64 * NSLOT;
-    for (int c = tid; c < (BPB * 64 + 1) * NSLOT; c += NT) {
+    for (int c = tid; c < BPB * 64 * NSLOT; c += NT) {
         const int rowi = c / NSLOT, slot = c - rowi * NSLOT;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (rowi < nb * 64) v = src[c];
-        const int sq = rowi & 63;
-        lds[rowi * NSLOT + (slot ^ (sq & SWZ))] = v;
+        lds[rowi * RS + slot] = rowi < nb * 64 ? src[c] : make_uint4(0, 0, 0, 0);
     }
+    for (int c = tid; c < ZN; c += NT) lds[ZB + c] = make_uint4(0, 0, 0, 0);
     __syncthreads();
 
     f32x4 acc[MF][2];
 #pragma unroll
     for (int m = 0; m < MF; m++) { acc[m][0] = f32x4{0, 0, 0, 0}; acc[m][1] = f32x4{0, 0, 0, 0}; }
 
-    const uint4* W = reinterpret_cast<const uint4*>(wsw);
+    const uint4* W = reinterpret_cast<const uint4*>(wsw) + (size_t)(w * 2) * 64 + lane;
     const int h = lane >> 4;
-    uint4 a0 = W[(0 * CF + w * 2 + 0) * 64 + lane];
-    uint4 a1 = W[(0 * CF + w * 2 + 1) * 64 + lane];
+    // weight fragments: register prefetch one k-step ahead (the buffer is padded by one k-step)
+    uint4 a0 = W[0], a1 = W[64];
     const char* ldsb = reinterpret_cast<const char*>(lds);
-    const int zero_row = BPB * 64 * NSLOT * 16;
 
     for (int tap = 0; tap < 9; tap++) {
         const int dr = tap / 3 - 1, df = tap % 3 - 1;
-        int base[MF], xm[MF];
+        int base[MF];
 #pragma unroll
         for (int m = 0; m < MF; m++) {
             const int b = m >> 2;
             const int sq = (m & 3) * 16 + (lane & 15);
             const int r = (sq >> 3) + dr, f = (sq & 7) + df;
             const bool ok = (unsigned)r < 8u && (unsigned)f < 8u;
-            const int s2 = r * 8 + f;
-            base[m] = ok ? (b * 64 + s2) * NSLOT * 16 : zero_row;
-            xm[m] = ok ? (s2 & SWZ) : 0;
+            const int s2 = (r * 8 + f) & 63;
+            // off-board lanes read zeros at the bank quad their wrapped square would use
+            base[m] = ok ? ((b * 64 + s2) * RS + h) * 16 : (ZB + ((s2 * RS) & 15) + h) * 16;
         }
 #pragma unroll
         for (int cc = 0; cc < NCH; cc++) {
             const int ks = tap * NCH + cc;
-            const uint4 n0 = W[((ks + 1) * CF + w * 2 + 0) * 64 + lane];   // +1 k-step padded
-            const uint4 n1 = W[((ks + 1) * CF + w * 2 + 1) * 64 + lane];
-            const int K = cc * 4 + h;
+            // next k-step's weight fragments: issued first so a whole k-step hides their latency
+            const uint4 n0 = W[(size_t)(ks + 1) * CF * 64], n1 = W[(size_t)(ks + 1) * CF * 64 + 64];
+            __builtin_amdgcn_sched_barrier(0);
+            constexpr int LA = 3;                    // LDS reads kept in flight
+            uint4 bq[LA];
+#pragma unroll
+            for (int m = 0; m < LA; m++) bq[m] = *reinterpret_cast<const uint4*>(ldsb + base[m] + cc * 64);
 #pragma unroll
             for (int m = 0; m < MF; m++) {
-                const uint4 bv = *reinterpret_cast<const uint4*>(ldsb + base[m] + ((K ^ xm[m]) << 4));
+                const uint4 bv = bq[m % LA];
+                if (m + LA < MF) bq[m % LA] = *reinterpret_cast<const uint4*>(ldsb + base[m + LA] + cc * 64);
                 if constexpr (sizeof(T) == 2) {
                     const bf16x8 A0 = __builtin_bit_cast(bf16x8, a0), A1 = __builtin_bit_cast(bf16x8, a1);
                     const bf16x8 Bv = __builtin_bit_cast(bf16x8, bv);
@@ -128,7 +132,16 @@ conv3x3_kernel(const T* __restrict__ in, T* __restrict__ out, const void* __rest
                     }
                 }
             }
+            // pin the interleave: LA reads ahead, then [1 ds_read, the fragment's MFMAs] per fragment
+            constexpr int MPM = sizeof(T) == 2 ? 2 : 8;
+            __builtin_amdgcn_sched_group_barrier(0x100, LA, 0);
+#pragma unroll
+            for (int m = 0; m < MF; m++) {
+                if (m + LA < MF) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, MPM, 0);
+            }
             a0 = n0; a1 = n1;
+            __builtin_amdgcn_sched_barrier(0);      // keep each k-step's reads with its MFMAs (no spills)
         }
     }
 

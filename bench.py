@@ -63,16 +63,15 @@ def main():
     ap.add_argument("--cpu-sims", type=int, default=8)
     args = ap.parse_args()
 
+    # libaz (and the /opt/rocm HIP runtime it is built for) is loaded before torch: torch
+    # bundles its own libamdhip64.so.7 (same SONAME) and is only used here for the gloo
+    # barrier / reduction between ranks -- the self-play path has no collective.
+    import azchess as A
     from azchess.dist import barrier as dist_barrier, env_rank, reduce_run, shard
     rank, world, local = env_rank()
-    import torch
-    import torch.distributed as dist
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    import azchess as A
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
 
     G, S = args.games, args.sims
     net = A.AlphaZero(args.blocks, args.filters, dtype=args.dtype, device=local, seed=42)
@@ -85,9 +84,12 @@ def main():
     st0 = sp.search.stats()
     sp.search.timing(reset=True, enable=True)
 
+    def synchronize():
+        A._lib.check(A._lib.lib.az_device_synchronize(local))
+
     def barrier():
         dist_barrier(world)
-        torch.cuda.synchronize()
+        synchronize()
 
     barrier()
     t0 = time.perf_counter()
@@ -96,7 +98,7 @@ def main():
         f, _ = sp.step()
         finished += f
         sp.drain()
-    torch.cuda.synchronize()
+    synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
     tm = sp.search.timing(reset=False, enable=False)
@@ -106,8 +108,7 @@ def main():
     term_rank = st1["terminal_leaves"] - st0["terminal_leaves"]
     moves_rank = st1["moves"] - st0["moves"]
     depth_rank = st1["max_depth_sum"] - st0["max_depth_sum"]
-    elapsed, tot = reduce_run(elapsed, [sims_rank, evals_rank, term_rank, finished, moves_rank, depth_rank], world,
-                              device="cuda")
+    elapsed, tot = reduce_run(elapsed, [sims_rank, evals_rank, term_rank, finished, moves_rank, depth_rank], world)
     sims_all, evals_all, term_all, fin_all, moves_all, depth_all = tot
     assert sims_rank == G * S * args.steps, (sims_rank, G * S * args.steps)
 
@@ -136,7 +137,7 @@ def main():
         "config": {"workload": "C3 (BASELINE.json configs[2]): %d concurrent self-play games/GPU x %d sims/move, "
                                "%d-block x %d-filter net" % (G, S, args.blocks, args.filters),
                    "games_per_gpu": G, "sims_per_move": S, "blocks": args.blocks, "filters": args.filters,
-                   "parallelism": "games sharded %d-way, no collective" % world},
+                   "parallelism": "games sharded %d-way, no collective (gloo barrier/max only)" % world},
         "roofline": {"bound": "mfma", "achieved": conv_tflops, "peak": peak, "unit": "TFLOP/s",
                      "frac": conv_tflops / peak, "traffic": None,
                      "kernel": "conv3x3_kernel<%d,%d> (residual 3x3 conv), %d launches timed" %

@@ -45,6 +45,7 @@ typedef struct az_pos {
 const char* az_last_error(void);
 int az_version(void);
 int az_device_count(int* n);
+int az_device_synchronize(int device);                              /* hipDeviceSynchronize on `device` */
 
 /* ---- rules & codec: chess.rs ---------------------------------------------------- */
 int az_pos_startpos(az_pos* out);                                   /* Chess::new, chess.rs:21 */
