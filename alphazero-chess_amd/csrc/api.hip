@@ -288,6 +288,10 @@ int az_net_forward_device(az_net* net, const float* d_planes, int rows, float* d
     hipStream_t st = stream ? (hipStream_t)stream : n->stream;
     int rc = ensure_scratch(n, rows);
     if (!rc) rc = net_planes_from_host_layout(n, d_planes, rows, n->planes, st);
+    if (n->fused && tower_supported(n)) {
+        if (!rc) rc = tower_forward(n, n->planes, nullptr, rows, d_policy, d_value, nullptr, st);
+        return rc;
+    }
     if (!rc) rc = net_tower(n, n->planes, nullptr, rows, n->x, n->h, st, nullptr, nullptr);
     if (!rc) rc = net_heads_dense(n, n->x, rows, d_policy, d_value, st);
     return rc;

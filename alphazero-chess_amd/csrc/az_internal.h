@@ -101,6 +101,7 @@ struct NetDev {
     float* head = nullptr;          // folded head weights (f32)
     size_t head_floats = 0;
     hipStream_t stream = nullptr;
+    bool fused = true;              // use tower_forward when supported (AZ_FUSED_TOWER=0 disables)
     // scratch for az_net_forward
     void* x = nullptr; void* h = nullptr; void* planes = nullptr; int scratch_rows = 0;
     float* d_in = nullptr; float* d_pol = nullptr; float* d_val = nullptr; int io_rows = 0;
@@ -148,6 +149,10 @@ int net_encode_rows(NetDev* n, const azc::Pos* npos, int NMAX, const int* row_ga
                     const int* count, int rows, void* planes, hipStream_t st);
 int synth_eval_rows(const int* count, int rows, const SearchOut& so, hipStream_t st);
 int net_planes_from_host_layout(NetDev* n, const float* d_in, int rows, void* planes, hipStream_t st);
+// fused tower (tower.hip): input conv + residual tower + heads in one launch, bf16 only.
+bool tower_supported(const NetDev* n);
+int tower_forward(NetDev* n, const void* planes, const int* count, int rows, float* pol, float* val,
+                  const SearchOut* so, hipStream_t st);
 size_t act_bytes(int dtype);
 double net_flop_per_eval(int blocks, int filters);
 double net_tower_flop_per_eval(int blocks, int filters);

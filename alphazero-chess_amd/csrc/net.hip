@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 
 #include "az_internal.h"
 
@@ -397,7 +398,7 @@ int launch_conv(int F, int cin, bool resid, const void* in, void* out, const voi
 // fragment-swizzle one folded conv weight [cout][cin_real][9] for the MFMA A operand
 std::vector<uint16_t> swizzle_bf16(const std::vector<float>& wf, int cout, int cin_real, int CIN) {
     const int nks = 9 * CIN / 32, CF = cout / 16;
-    std::vector<uint16_t> o((size_t)(nks + 1) * CF * 64 * 8, 0);
+    std::vector<uint16_t> o((size_t)(nks + 2) * CF * 64 * 8, 0);   // 2 zero k-steps of prefetch padding
     for (int ks = 0; ks < nks; ks++)
         for (int cf = 0; cf < CF; cf++)
             for (int lane = 0; lane < 64; lane++)
@@ -415,7 +416,7 @@ std::vector<uint16_t> swizzle_bf16(const std::vector<float>& wf, int cout, int c
 }
 std::vector<float> swizzle_f32(const std::vector<float>& wf, int cout, int cin_real, int CIN) {
     const int nkc = 9 * CIN / 16, CF = cout / 16;
-    std::vector<float> o((size_t)(nkc + 1) * CF * 64 * 4, 0.0f);
+    std::vector<float> o((size_t)(nkc + 2) * CF * 64 * 4, 0.0f);
     for (int kc = 0; kc < nkc; kc++)
         for (int cf = 0; cf < CF; cf++)
             for (int lane = 0; lane < 64; lane++)
@@ -440,6 +441,7 @@ int net_create(const az_net_desc* d, const float* wts, size_t n, int device, Net
     AZ_HIP(hipSetDevice(device));
     NetDev* net = new NetDev();
     net->blocks = B; net->filters = F; net->dtype = d->dtype; net->device = device;
+    if (const char* e = getenv("AZ_FUSED_TOWER")) net->fused = atoi(e) != 0;
     AZ_HIP(hipStreamCreateWithFlags(&net->stream, hipStreamNonBlocking));
     const float* p = wts;
     auto fold_conv = [&](int cin, const float* w, const float* bias, const float* bn) {

@@ -504,11 +504,19 @@ int sim_step(az_search* s, int step, hipEvent_t* ev) {
         rc = net_encode_rows(n, E.npos, E.NMAX, E.row_game, E.row_node, cnt, G, s->planes, st);
         if (rc) return rc;
         if (ev) (void)hipEventRecord(ev[3], st);
-        rc = net_tower(n, s->planes, cnt, G, s->x, s->h, st, ev ? ev[7] : nullptr, ev ? ev[8] : nullptr);
-        if (rc) return rc;
-        if (ev) (void)hipEventRecord(ev[4], st);
-        rc = net_heads_search(n, s->x, cnt, G, s->so, st);
-        if (rc) return rc;
+        if (n->fused && tower_supported(n)) {
+            // one launch: 41 convs + heads, activations resident in LDS
+            if (ev) (void)hipEventRecord(ev[7], st);
+            rc = tower_forward(n, s->planes, cnt, G, nullptr, nullptr, &s->so, st);
+            if (rc) return rc;
+            if (ev) { (void)hipEventRecord(ev[8], st); (void)hipEventRecord(ev[4], st); }
+        } else {
+            rc = net_tower(n, s->planes, cnt, G, s->x, s->h, st, ev ? ev[7] : nullptr, ev ? ev[8] : nullptr);
+            if (rc) return rc;
+            if (ev) (void)hipEventRecord(ev[4], st);
+            rc = net_heads_search(n, s->x, cnt, G, s->so, st);
+            if (rc) return rc;
+        }
     } else {
         if (ev) { (void)hipEventRecord(ev[3], st); (void)hipEventRecord(ev[7], st); (void)hipEventRecord(ev[8], st); }
         if (ev) (void)hipEventRecord(ev[4], st);
@@ -528,6 +536,10 @@ int eval_rows(az_search* s) {
     if (s->cfg.evaluator == AZ_EVAL_NET) {
         NetDev* n = s->net->dev;
         int rc = net_encode_rows(n, E.npos, E.NMAX, E.row_game, E.row_node, cnt, E.G, s->planes, s->st);
+        if (n->fused && tower_supported(n)) {
+            if (!rc) rc = tower_forward(n, s->planes, cnt, E.G, nullptr, nullptr, &s->so, s->st);
+            return rc;
+        }
         if (!rc) rc = net_tower(n, s->planes, cnt, E.G, s->x, s->h, s->st, nullptr, nullptr);
         if (!rc) rc = net_heads_search(n, s->x, cnt, E.G, s->so, s->st);
         return rc;
@@ -557,6 +569,7 @@ int run_sims(az_search* s) {
         const double F = net ? s->net->dev->filters : 0.0;
         const double per_row_conv = 2.0 * 64.0 * 9.0 * F * F;
         const double per_row_tower = net ? net_tower_flop_per_eval(s->net->dev->blocks, s->net->dev->filters) : 0.0;
+        const bool fused = net && s->net->dev->fused && tower_supported(s->net->dev);
         for (int i = 0; i < S; i++) {
             hipEvent_t* e = &s->ev[EV_PER_STEP * i];
             float t[6], tc = 0.0f;
@@ -574,7 +587,7 @@ int run_sims(az_search* s) {
             a.rows += rows[i];
             if (net && rows[i] > 0 && s->net->dev->blocks > 0) {
                 a.conv_ms += tc; a.conv_launches++;
-                a.conv_flop += per_row_conv * rows[i];
+                a.conv_flop += (fused ? per_row_tower : per_row_conv) * rows[i];
             }
             a.tower_flop += per_row_tower * rows[i];
         }

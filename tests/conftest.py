@@ -9,6 +9,14 @@ for p in (os.path.join(ROOT, "alphazero-chess_amd"), os.path.join(ROOT, "oracle"
         sys.path.insert(0, p)
 
 
+# Bind libaz to the /opt/rocm HIP runtime it is built for before anything imports torch
+# (torch bundles a libamdhip64.so.7 with the same SONAME).
+try:
+    import azchess  # noqa: F401,E402
+except ImportError:
+    pass
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libaz on cuda:0)")
 

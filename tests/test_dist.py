@@ -3,8 +3,6 @@ bench.py uses (no GPU; the self-play path itself has no collective)."""
 import os
 import socket
 
-import pytest
-import torch.multiprocessing as mp
 
 
 def _free_port():
@@ -33,6 +31,7 @@ def _worker(rank, world, port, q):
 
 
 def test_two_rank_gloo_sharding_and_reduction():
+    import torch.multiprocessing as mp
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

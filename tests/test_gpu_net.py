@@ -78,3 +78,19 @@ def test_rows_are_batch_independent(require_gpu, dtype):
         assert np.array_equal(p1[0], pol[i]) and v1[0] == val[i]
     p2, v2 = net.forward(np.concatenate([planes[7:], planes[:7]]))
     assert np.array_equal(p2[:6], pol[7:]) and np.array_equal(v2[6:], val[:7])
+
+
+@pytest.mark.parametrize("blocks,filters", [(2, 32), (6, 64), (2, 128), (20, 256)])
+def test_fused_tower_matches_per_layer_kernels(require_gpu, blocks, filters, monkeypatch):
+    """tower_kernel (whole tower + heads in one launch, activations resident in LDS) against
+    the per-layer conv3x3_kernel + heads_kernel path on the same bf16 weights."""
+    w = A.random_weights(blocks, filters, seed=7)
+    planes = random_planes(37, 11)
+    monkeypatch.setenv("AZ_FUSED_TOWER", "1")
+    fused = A.AlphaZero(blocks, filters, weights=w, dtype="bf16")
+    pf, vf = fused.forward(planes)
+    monkeypatch.setenv("AZ_FUSED_TOWER", "0")
+    layered = A.AlphaZero(blocks, filters, weights=w, dtype="bf16")
+    pl, vl = layered.forward(planes)
+    np.testing.assert_allclose(vf, vl, atol=1e-5)
+    np.testing.assert_allclose(pf, pl, rtol=1e-4, atol=1e-8)
