@@ -31,7 +31,7 @@ class AzSearchCfg(C.Structure):
     _fields_ = [("games", C.c_int), ("sims", C.c_int), ("c_puct", C.c_float), ("dir_alpha", C.c_float),
                 ("dir_eps", C.c_float), ("temp_moves", C.c_int), ("noise", C.c_int), ("seed", C.c_uint64),
                 ("evaluator", C.c_int), ("continuous", C.c_int), ("record_evals", C.c_int),
-                ("eval_log_cap", C.c_int)]
+                ("eval_log_cap", C.c_int), ("cache_capacity", C.c_int)]
 
 
 class AzEpisodeStep(C.Structure):
@@ -42,7 +42,8 @@ class AzEpisodeStep(C.Structure):
 
 class AzSearchStats(C.Structure):
     _fields_ = [("sims", C.c_int64), ("evals", C.c_int64), ("terminal_leaves", C.c_int64),
-                ("games_finished", C.c_int64), ("moves", C.c_int64), ("max_depth_sum", C.c_int64)]
+                ("games_finished", C.c_int64), ("moves", C.c_int64), ("max_depth_sum", C.c_int64),
+                ("cache_hits", C.c_int64), ("cache_misses", C.c_int64)]
 
 
 class AzTiming(C.Structure):

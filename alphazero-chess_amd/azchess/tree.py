@@ -8,15 +8,15 @@ import ctypes as C
 import numpy as np
 
 from . import _lib as L
-from .parameters import C_PUCT, DIRICHLET_ALPHA, DIRICHLET_EPSILON, NUM_SIMULATIONS, SEED, TEMPERATURE_ANNEALING
+from .parameters import CACHE_CAPACITY, C_PUCT, DIRICHLET_ALPHA, DIRICHLET_EPSILON, NUM_SIMULATIONS, SEED, TEMPERATURE_ANNEALING
 
 
 def make_cfg(games, sims=NUM_SIMULATIONS, c_puct=C_PUCT, dir_alpha=DIRICHLET_ALPHA, dir_eps=DIRICHLET_EPSILON,
              temp_moves=TEMPERATURE_ANNEALING, noise=True, seed=SEED, synthetic=False, continuous=False,
-             record_evals=False, eval_log_cap=0):
+             record_evals=False, eval_log_cap=0, cache_capacity=CACHE_CAPACITY):
     return L.AzSearchCfg(games, sims, c_puct, dir_alpha, dir_eps, temp_moves, 1 if noise else 0, seed,
                          L.EVAL_SYNTHETIC if synthetic else L.EVAL_NET, 1 if continuous else 0,
-                         1 if record_evals else 0, eval_log_cap)
+                         1 if record_evals else 0, eval_log_cap, cache_capacity)
 
 
 class BatchedSearch:

@@ -40,7 +40,7 @@ struct Edge {            // 16 B, one dwordx4 per lane in the select walk
 };
 static_assert(sizeof(Node) == 16 && sizeof(Edge) == 16, "tree record layout");
 enum { CHILD_NONE = -1, CHILD_DRAW = -2, CHILD_WIN = -3 };
-enum { LEAF_EVAL = 0, LEAF_DRAW = 1, LEAF_WIN = 2 };
+enum { LEAF_EVAL = 0, LEAF_DRAW = 1, LEAF_WIN = 2, LEAF_CACHED = 3 };
 constexpr int MAX_EDGES = 224;     // >= 218 legal moves
 constexpr int HMAX = 512;          // game history cap (200 fullmoves -> <= 400 plies)
 
@@ -57,7 +57,7 @@ struct StepRec {                   // device -> host self-play record, 1024 B
 static_assert(sizeof(StepRec) == 1024, "StepRec");
 
 struct Counters {                  // device-side statistics
-    unsigned long long sims, evals, terminal, games_finished, moves, depth_sum, select_bytes;
+    unsigned long long sims, evals, terminal, games_finished, moves, depth_sum, select_bytes, cache_hits;
     int batch_count;
     int rec_count;
     int next_game_id;
@@ -88,6 +88,15 @@ struct Engine {
     StepRec* recs; int rec_cap;
     Counters* ctr;
     int* batch_hist;                       // [S] rows evaluated per sim step
+    // FEN evaluation cache (tree.rs:214-219): open addressing, CACHE_PROBES linear probes
+    int cache_mask;                        // slots - 1 (slots = power of two), -1 = off
+    unsigned* c_state;                     // 0 empty, 1 being written, 2 valid
+    unsigned long long* c_key;
+    azc::Pos* c_pos;
+    float* c_value;
+    int* c_n;
+    float* c_pri;                          // [slots][MAX_EDGES]
+    float* cached_value;                   // [G] value of a cache-served leaf
     // evaluation log
     int log_cap, log_prior_cap;
     unsigned long long* log_key; float* log_value; int* log_off; int* log_n; int* log_idx; float* log_prior;

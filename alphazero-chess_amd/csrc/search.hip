@@ -85,6 +85,46 @@ __global__ void __launch_bounds__(256) k_select(Engine E) {
     }
 }
 
+// ------------------------------------------------------------------ FEN cache
+constexpr int CACHE_PROBES = 4;
+
+__device__ __forceinline__ bool same_fen(const azc::Pos& a, const azc::Pos& b) {   // FEN(PseudoLegal) equality
+    for (int i = 0; i < 8; i++) if (a.bb[i] != b.bb[i]) return false;
+    return a.turn == b.turn && a.castling == b.castling && a.ep == b.ep && a.halfmoves == b.halfmoves &&
+           a.fullmoves == b.fullmoves;
+}
+
+// insert every row just evaluated by the network (process_batch's cache.insert, training.rs:413)
+__global__ void __launch_bounds__(64) k_cache_insert(Engine E) {
+    const int row = blockIdx.x * blockDim.x + threadIdx.x;
+    if (row >= E.ctr->batch_count) return;
+    const int g = E.row_game[row], node = E.row_node[row];
+    const azc::Pos p = E.npos[(size_t)g * E.NMAX + node];
+    const Node nd = E.nodes[(size_t)g * E.NMAX + node];
+    const Edge* edges = E.edges + (size_t)g * E.EMAX + nd.edge_begin;
+    const uint64_t key = azc::fen_key(p);
+    int sl = -1;
+    for (int i = 0; i < CACHE_PROBES && sl < 0; i++) {
+        const int s = (int)((key + (uint64_t)i) & (uint64_t)E.cache_mask);
+        const unsigned st = E.c_state[s];
+        if (st == 2u && E.c_key[s] == key && same_fen(E.c_pos[s], p)) return;   // already cached
+        if (st == 0u && atomicCAS(&E.c_state[s], 0u, 1u) == 0u) sl = s;
+    }
+    if (sl < 0) {                                            // all probes taken: replace the first
+        const int s = (int)(key & (uint64_t)E.cache_mask);
+        if (atomicCAS(&E.c_state[s], 2u, 1u) != 2u) return;  // another row is writing it: skip
+        sl = s;
+    }
+    E.c_key[sl] = key;
+    E.c_pos[sl] = p;
+    E.c_value[sl] = E.value[row];
+    E.c_n[sl] = nd.nedges;
+    float* pri = E.c_pri + (size_t)sl * MAX_EDGES;
+    for (int e = 0; e < nd.nedges; e++) pri[e] = edges[e].P;
+    __threadfence();
+    atomicExch(&E.c_state[sl], 2u);
+}
+
 // ------------------------------------------------------------------ expand
 struct EdgeSink {
     Edge* out;
@@ -150,6 +190,19 @@ __global__ void __launch_bounds__(64) k_expand(Engine E) {
     E.edge_count[g] = ebeg + n;
     edges[eabs].child = nid;
     if (nn.depth > E.max_depth[g]) E.max_depth[g] = nn.depth;
+    if (E.cache_mask >= 0) {                                 // FEN cache lookup (tree.rs:214-219)
+        const uint64_t key = azc::fen_key(c);
+        for (int i = 0; i < CACHE_PROBES; i++) {
+            const int sl = (int)((key + (uint64_t)i) & (uint64_t)E.cache_mask);
+            if (E.c_state[sl] != 2u || E.c_key[sl] != key || E.c_n[sl] != n || !same_fen(E.c_pos[sl], c)) continue;
+            const float* pri = E.c_pri + (size_t)sl * MAX_EDGES;
+            for (int e = 0; e < n; e++) edges[ebeg + e].P = pri[e];
+            E.cached_value[g] = E.c_value[sl];
+            E.leaf_kind[g] = LEAF_CACHED;
+            atomicAdd(&E.ctr->cache_hits, 1ull);
+            return;
+        }
+    }
     const int row = atomicAdd(&E.ctr->batch_count, 1);
     E.row_game[row] = g;
     E.row_node[row] = nid;
@@ -168,7 +221,8 @@ __global__ void __launch_bounds__(256) k_backup(Engine E, int step) {
     Node* nodes = game_nodes(E, g);
     Edge* edges = game_edges(E, g);
     const int kind = E.leaf_kind[g], len = E.leaf_len[g];
-    const float v = kind == LEAF_EVAL ? E.value[E.leaf_row[g]] : (kind == LEAF_DRAW ? 0.0f : -1.0f);
+    const float v = kind == LEAF_EVAL ? E.value[E.leaf_row[g]]
+                  : kind == LEAF_CACHED ? E.cached_value[g] : (kind == LEAF_DRAW ? 0.0f : -1.0f);
     const int* pn = E.path_node + (size_t)g * E.PMAX;
     const int* pe = E.path_edge + (size_t)g * E.PMAX;
     for (int k = lane; k < len; k += 64) {
@@ -523,6 +577,7 @@ int sim_step(az_search* s, int step, hipEvent_t* ev) {
         rc = synth_eval_rows(cnt, G, s->so, st);
         if (rc) return rc;
     }
+    if (E.cache_mask >= 0) k_cache_insert<<<(G + 63) / 64, 64, 0, st>>>(E);
     if (ev) (void)hipEventRecord(ev[5], st);
     k_backup<<<(G * 64 + 255) / 256, 256, 0, st>>>(E, step);
     if (ev) (void)hipEventRecord(ev[6], st);
@@ -704,6 +759,7 @@ int az_search_default_cfg(az_search_cfg* c) {
     c->continuous = 0;
     c->record_evals = 0;
     c->eval_log_cap = 0;
+    c->cache_capacity = 500000;   // CACHE_CAPACITY parameters.rs:4
     return 0;
 }
 
@@ -741,6 +797,16 @@ int az_search_create(az_net* net, const az_search_cfg* cfg, int device, az_searc
     rc |= dalloc(s, &E.recs, E.rec_cap);
     rc |= dalloc(s, &E.ctr, 1);
     rc |= dalloc(s, &E.batch_hist, S);
+    rc |= dalloc(s, &E.cached_value, G);
+    E.cache_mask = -1;
+    if (cfg->cache_capacity > 0) {
+        int slots = 1;
+        while (slots < cfg->cache_capacity) slots <<= 1;
+        E.cache_mask = slots - 1;
+        rc |= dalloc(s, &E.c_state, slots); rc |= dalloc(s, &E.c_key, slots); rc |= dalloc(s, &E.c_pos, slots);
+        rc |= dalloc(s, &E.c_value, slots); rc |= dalloc(s, &E.c_n, slots);
+        rc |= dalloc(s, &E.c_pri, (size_t)slots * MAX_EDGES);
+    }
     if (rc) { az_search_destroy(s); return -1; }
     std::vector<float> st(S + 2);
     for (int i = 0; i < S + 2; i++) st[i] = sqrtf((float)i);    // f32 sqrt, correctly rounded
@@ -845,6 +911,7 @@ int az_selfplay_reset(az_search* s) {
     int rc = upload_histories(s, nullptr, nullptr, nullptr, nullptr);
     if (rc) return rc;
     AZ_HIP(hipMemset(s->E.ctr, 0, sizeof(Counters)));
+    if (s->E.cache_mask >= 0) AZ_HIP(hipMemset(s->E.c_state, 0, (size_t)(s->E.cache_mask + 1) * sizeof(unsigned)));
     const int G = s->E.G;
     AZ_HIP(hipMemcpy(&s->E.ctr->next_game_id, &G, 4, hipMemcpyHostToDevice));
     s->pending.clear();
@@ -901,6 +968,8 @@ int az_search_stats_get(az_search* s, az_search_stats* out) {
     out->games_finished = (int64_t)c.games_finished;
     out->moves = (int64_t)c.moves;
     out->max_depth_sum = (int64_t)c.depth_sum;
+    out->cache_hits = (int64_t)c.cache_hits;
+    out->cache_misses = (int64_t)c.evals;
     return 0;
 }
 

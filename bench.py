@@ -57,6 +57,7 @@ def main():
     ap.add_argument("--blocks", type=int, default=20)
     ap.add_argument("--filters", type=int, default=256)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--cache", type=int, default=500000, help="FEN cache entries (CACHE_CAPACITY, 0 = off)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-games", type=int, default=16)
@@ -76,13 +77,6 @@ def main():
     G, S = args.games, args.sims
     net = A.AlphaZero(args.blocks, args.filters, dtype=args.dtype, device=local, seed=42)
     sh = shard(rank, world, G)
-    sp = A.SelfPlay(net, games=G, sims=S, device=local, continuous=True, seed=sh["seed"])
-    sp.reset()
-    for _ in range(args.warmup):
-        sp.step()
-        sp.drain()
-    st0 = sp.search.stats()
-    sp.search.timing(reset=True, enable=True)
 
     def synchronize():
         A._lib.check(A._lib.lib.az_device_synchronize(local))
@@ -91,26 +85,45 @@ def main():
         dist_barrier(world)
         synchronize()
 
-    barrier()
-    t0 = time.perf_counter()
-    finished = 0
-    for _ in range(args.steps):
-        f, _ = sp.step()
-        finished += f
-        sp.drain()
-    synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    tm = sp.search.timing(reset=False, enable=False)
-    st1 = sp.search.stats()
-    sims_rank = st1["sims"] - st0["sims"]
-    evals_rank = st1["evals"] - st0["evals"]
-    term_rank = st1["terminal_leaves"] - st0["terminal_leaves"]
-    moves_rank = st1["moves"] - st0["moves"]
-    depth_rank = st1["max_depth_sum"] - st0["max_depth_sum"]
-    elapsed, tot = reduce_run(elapsed, [sims_rank, evals_rank, term_rank, finished, moves_rank, depth_rank], world)
-    sims_all, evals_all, term_all, fin_all, moves_all, depth_all = tot
-    assert sims_rank == G * S * args.steps, (sims_rank, G * S * args.steps)
+    def phase(cache, steps, timing):
+        """Self-play from startpos: warmup moves, then `steps` timed moves of every game."""
+        sp = A.SelfPlay(net, games=G, sims=S, device=local, continuous=True, seed=sh["seed"], cache_capacity=cache)
+        sp.reset()
+        for _ in range(args.warmup):
+            sp.step()
+            sp.drain()
+        st0 = sp.search.stats()
+        sp.search.timing(reset=True, enable=timing)
+        barrier()
+        t0 = time.perf_counter()
+        finished = 0
+        for _ in range(steps):
+            f, _ = sp.step()
+            finished += f
+            sp.drain()
+        synchronize()
+        barrier()
+        elapsed = time.perf_counter() - t0
+        tm = sp.search.timing(reset=False, enable=False)
+        st1 = sp.search.stats()
+        c = [st1[k] - st0[k] for k in ("sims", "evals", "terminal_leaves", "moves", "max_depth_sum", "cache_hits")]
+        assert c[0] == G * S * steps, (c[0], G * S * steps)
+        elapsed, tot = reduce_run(elapsed, c + [finished], world)
+        del sp
+        return elapsed, dict(zip(("sims", "evals", "terminal", "moves", "depth", "hits", "finished"), tot)), tm, c[0]
+
+    # headline: no FEN cache -> every non-terminal simulation evaluates its leaf on the network
+    elapsed, tot, tm, sims_rank = phase(0, args.steps, True)
+    sims_all, evals_all, term_all = tot["sims"], tot["evals"], tot["terminal"]
+    fin_all, moves_all, depth_all = tot["finished"], tot["moves"], tot["depth"]
+    # the reference's FEN cache (tree.rs:214-219, CACHE_CAPACITY = 500k) on the same window
+    cache_res = None
+    if args.cache > 0:
+        e2, t2, _, _ = phase(args.cache, args.steps, False)
+        cache_res = {"value": t2["sims"] / e2, "unit": "sims/s", "evals_per_sim": t2["evals"] / max(t2["sims"], 1),
+                     "cache_hit_frac": t2["hits"] / max(t2["sims"], 1), "entries": args.cache,
+                     "note": "same window with the reference's FEN evaluation cache (A12); games are in "
+                             "lockstep from startpos, so early moves share most positions"}
 
     if rank != 0:
         dist.destroy_process_group()
@@ -137,6 +150,7 @@ def main():
         "config": {"workload": "C3 (BASELINE.json configs[2]): %d concurrent self-play games/GPU x %d sims/move, "
                                "%d-block x %d-filter net" % (G, S, args.blocks, args.filters),
                    "games_per_gpu": G, "sims_per_move": S, "blocks": args.blocks, "filters": args.filters,
+                   "fen_cache": "off for value (see with_fen_cache)",
                    "parallelism": "games sharded %d-way, no collective (gloo barrier/max only)" % world},
         "roofline": {"bound": "mfma", "achieved": conv_tflops, "peak": peak, "unit": "TFLOP/s",
                      "frac": conv_tflops / peak, "traffic": None,
@@ -154,6 +168,7 @@ def main():
                         for k in ("select", "expand", "encode", "tower", "heads", "backup")},
         "evals_per_sim": evals_all / max(sims_all, 1),
         "terminal_leaf_frac": term_all / max(sims_all, 1),
+        "with_fen_cache": cache_res,
         "avg_search_depth": depth_all / max(moves_all, 1),
         "games_finished": int(fin_all),
         "games_per_hr": fin_all / elapsed * 3600.0,

@@ -108,6 +108,9 @@ typedef struct {
     int continuous;     /* self-play: restart a finished slot with a new game */
     int record_evals;   /* keep a log of every evaluation (for replay parity) */
     int eval_log_cap;   /* log capacity in rows */
+    int cache_capacity; /* FEN evaluation cache entries (CACHE_CAPACITY, parameters.rs:4; 0 = off):
+                           tree.rs:214-219 lookup, training.rs:413 insert.  Changes only how many
+                           network rows run, never a result. */
 } az_search_cfg;
 typedef struct az_search az_search;
 
@@ -155,6 +158,8 @@ typedef struct {
     int64_t games_finished;
     int64_t moves;
     int64_t max_depth_sum;     /* sum over moves of max_subtree_depth */
+    int64_t cache_hits;        /* expansions served by the FEN cache (CACHE_HITS, training.rs:12) */
+    int64_t cache_misses;      /* expansions that needed a network row (CACHE_MISSES) */
 } az_search_stats;
 int az_search_stats_get(az_search* s, az_search_stats* out);
 

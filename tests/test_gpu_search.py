@@ -122,4 +122,35 @@ def test_large_batch_invariants(require_gpu):
     assert np.all(vis.sum(1) == S)
     assert np.allclose(imp.sum(1), 1.0, atol=1e-6)
     st = s.stats()
-    assert st["sims"] == G * S and st["evals"] == st["sims"] - st["terminal_leaves"]
+    assert st["sims"] == G * S and st["evals"] + st["cache_hits"] == st["sims"] - st["terminal_leaves"]
+
+
+def test_fen_cache_changes_only_the_eval_count(require_gpu):
+    """tree.rs:214-219: a cache hit returns exactly what the network would return, so the
+    games are identical with the cache on or off; only the number of network rows drops."""
+    games, sims = 8, 32
+    net = A.AlphaZero(2, 32, dtype="bf16")
+    runs = {}
+    for cap in (0, 500000):
+        sp = A.SelfPlay(net, games=games, sims=sims, seed=21, cache_capacity=cap)
+        sp.reset()
+        for _ in range(12):
+            sp.step()
+        st = sp.search.stats()
+        runs[cap] = (st, [(s.game_id, s.ply, s.action, tuple(sorted(s.visits.items()))) for s in sp.drain()])
+    (st0, s0), (st1, s1) = runs[0], runs[500000]
+    assert st0["sims"] == st1["sims"]
+    assert st1["cache_hits"] > 0 and st1["evals"] < st0["evals"]
+    assert st1["evals"] + st1["cache_hits"] == st0["evals"]
+
+
+def test_fen_cache_search_bit_exact(require_gpu):
+    hs = histories(16, 77)
+    s = A.BatchedSearch(None, games=len(hs), sims=200, noise=True, seed=4, cache_capacity=1 << 16)
+    s.set_roots(hs, apply_noise=True)
+    imp, vis, dep = s.run()
+    assert s.stats()["cache_hits"] > 0
+    cfg = O.make_cfg(sims=200, noise=True, seed=4, eval_kind=0)
+    for g, h in enumerate(hs):
+        rv, ri, rd, _ = O.search_game(cfg, h, noise=True, noise_key=O.lib().ref_stream_key(4, g, len(h), 0))
+        assert np.array_equal(vis[g].astype(np.float32), rv) and dep[g] == rd
