@@ -8,6 +8,7 @@ gamma=1, beta=0, running mean 0, var 1, plus a seeded 1e-2 perturbation so that 
 is exercised.
 """
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -70,6 +71,8 @@ class AlphaZero:
         h = C.c_void_p()
         L.check(L.lib.az_net_create(C.byref(desc), L.fptr(self.weights), self.weights.size, device, C.byref(h)))
         self._h = h
+        # libaz runs the fused tower kernel for bf16 nets unless AZ_FUSED_TOWER=0
+        self.fused_tower = dtype == "bf16" and os.environ.get("AZ_FUSED_TOWER", "1") != "0"
 
     def __del__(self):
         try:

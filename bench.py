@@ -154,7 +154,11 @@ def main():
                    "parallelism": "games sharded %d-way, no collective (gloo barrier/max only)" % world},
         "roofline": {"bound": "mfma", "achieved": conv_tflops, "peak": peak, "unit": "TFLOP/s",
                      "frac": conv_tflops / peak, "traffic": None,
-                     "kernel": "conv3x3_kernel<%d,%d> (residual 3x3 conv), %d launches timed" %
+                     "kernel": ("tower_kernel<%d> (fused input conv + %d residual convs + heads; algorithmic "
+                                "FLOPs = conv FLOPs only), %d launches timed" % (args.filters, 2 * args.blocks,
+                                                                                 tm["conv_launches"]))
+                               if net.fused_tower else
+                               "conv3x3_kernel<%d,%d> (residual 3x3 conv), %d launches timed" %
                                (args.filters, args.filters, tm["conv_launches"]),
                      "flop_per_launch": tm["conv_flop"] / max(tm["conv_launches"], 1),
                      "avg_ms_per_launch": tm["conv_ms"] / max(tm["conv_launches"], 1)},
