@@ -398,7 +398,7 @@ int launch_conv(int F, int cin, bool resid, const void* in, void* out, const voi
 // fragment-swizzle one folded conv weight [cout][cin_real][9] for the MFMA A operand
 std::vector<uint16_t> swizzle_bf16(const std::vector<float>& wf, int cout, int cin_real, int CIN) {
     const int nks = 9 * CIN / 32, CF = cout / 16;
-    std::vector<uint16_t> o((size_t)(nks + 2) * CF * 64 * 8, 0);   // 2 zero k-steps of prefetch padding
+    std::vector<uint16_t> o((size_t)(nks + 8) * CF * 64 * 8, 0);   // zero k-steps of prefetch padding
     for (int ks = 0; ks < nks; ks++)
         for (int cf = 0; cf < CF; cf++)
             for (int lane = 0; lane < 64; lane++)
@@ -416,7 +416,7 @@ std::vector<uint16_t> swizzle_bf16(const std::vector<float>& wf, int cout, int c
 }
 std::vector<float> swizzle_f32(const std::vector<float>& wf, int cout, int cin_real, int CIN) {
     const int nkc = 9 * CIN / 16, CF = cout / 16;
-    std::vector<float> o((size_t)(nkc + 2) * CF * 64 * 4, 0.0f);
+    std::vector<float> o((size_t)(nkc + 8) * CF * 64 * 4, 0.0f);
     for (int kc = 0; kc < nkc; kc++)
         for (int cf = 0; cf < CF; cf++)
             for (int lane = 0; lane < 64; lane++)

@@ -15,6 +15,10 @@
 
 #include "az_internal.h"
 
+#ifndef AZ_TOWER_PF
+#define AZ_TOWER_PF 2      // weight prefetch depth in k-steps (L2 latency cover; 4 measured no faster)
+#endif
+
 namespace azi {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
@@ -46,24 +50,52 @@ __device__ __forceinline__ float t_wave_sum(float v) {
 // One 3x3 conv layer LDS -> LDS.  IN: CIN channels, row stride RSI slots; OUT: F channels,
 // row stride RSO slots.  Wave (cw, bw) computes channels [32cw, 32cw+32) of boards
 // [bw*BPW, (bw+1)*BPW).  RESID: out = relu(conv(in) + bias + out).
+template <int NCH> struct RingPF { static constexpr int PF = NCH >= AZ_TOWER_PF ? AZ_TOWER_PF : NCH; };
+
+// Load k-steps [0, PF) of a layer's weight fragments into the ring.
+template <int NCH, int F>
+__device__ __forceinline__ void ring_fill(uint4 (&wr)[RingPF<NCH>::PF][2], const uint4* __restrict__ wsw, int cw,
+                                          int lane) {
+    constexpr int CF = F / 16;
+    const uint4* W = wsw + (size_t)(cw * 2) * 64 + lane;
+#pragma unroll
+    for (int i = 0; i < RingPF<NCH>::PF; i++) { wr[i][0] = W[(size_t)i * CF * 64]; wr[i][1] = W[(size_t)i * CF * 64 + 64]; }
+}
+
+// wr: register ring holding this layer's next PF weight k-steps on entry; on exit it holds
+// the first PF k-steps of `wnext` (the next layer with the same chunk count), or zeros.
 template <int CIN, int RSI, int F, int RSO, int BPW, bool RESID>
 __device__ __forceinline__ void conv_lds(const char* __restrict__ ldsb, uint4* __restrict__ out_lds, int in_off,
-                                         int zero_off, const uint4* __restrict__ wsw, const float* __restrict__ bias,
+                                         int zero_off, const uint4* __restrict__ wsw, const uint4* __restrict__ wnext,
+                                         const float* __restrict__ bias, uint4 (&wr)[RingPF<CIN / 32>::PF][2],
                                          int cw, int bw, int lane) {
     constexpr int NCH = CIN / 32;                     // 32-channel K chunks (4 slots)
     constexpr int CF = F / 16;
     constexpr int MF = BPW * 4;
     constexpr int KS = 9 * NCH;
+    // weight fragments are prefetched PF k-steps ahead through a register ring; PF divides
+    // NCH so the ring slot of every k-step is a compile-time constant
+    constexpr int PF = RingPF<NCH>::PF;
+    static_assert(NCH % PF == 0, "prefetch depth must divide the chunk count");
     const int h = lane >> 4;
+    // accumulators start at the folded bias: no bias adds in the epilogue
+    const float4 bias0 = *reinterpret_cast<const float4*>(bias + cw * 32 + h * 4);
+    const float4 bias1 = *reinterpret_cast<const float4*>(bias + cw * 32 + 16 + h * 4);
     f32x4 acc[MF][2];
 #pragma unroll
-    for (int m = 0; m < MF; m++) { acc[m][0] = f32x4{0, 0, 0, 0}; acc[m][1] = f32x4{0, 0, 0, 0}; }
+    for (int m = 0; m < MF; m++) {
+        acc[m][0] = f32x4{bias0.x, bias0.y, bias0.z, bias0.w};
+        acc[m][1] = f32x4{bias1.x, bias1.y, bias1.z, bias1.w};
+    }
     const uint4* W = wsw + (size_t)(cw * 2) * 64 + lane;
-    uint4 a0 = W[0], a1 = W[64];
-    uint4 p0 = W[(size_t)CF * 64], p1 = W[(size_t)CF * 64 + 64];
-    for (int tap = 0; tap < 9; tap++) {
+    // past the last k-step the refills read the next layer (or this layer's zero padding)
+    const uint4* Wn = (wnext ? wnext + (size_t)(cw * 2) * 64 + lane : W + (size_t)KS * CF * 64) - (size_t)KS * CF * 64;
+    // B-fragment (activation) reads run LA fragments ahead, across k-step and tap boundaries:
+    // the first LA reads of step s+1 are issued inside step s.
+    constexpr int LA = 4;
+    static_assert(MF % LA == 0, "read-ahead ring must tile the fragment loop");
+    auto tap_bases = [&](int tap, int* base) {
         const int dr = tap / 3 - 1, df = tap % 3 - 1;
-        int base[MF];
 #pragma unroll
         for (int m = 0; m < MF; m++) {
             const int b = bw * BPW + (m >> 2);
@@ -73,59 +105,76 @@ __device__ __forceinline__ void conv_lds(const char* __restrict__ ldsb, uint4* _
             const int s2 = (r * 8 + f) & 63;
             base[m] = ok ? in_off + ((b * 64 + s2) * RSI + h) * 16 : zero_off + (((s2 * RSI) & 15) + h) * 16;
         }
+    };
+    int bcur[MF], bnext[MF];
+    tap_bases(0, bcur);
+    uint4 bq[LA];
+#pragma unroll
+    for (int m = 0; m < LA; m++) bq[m] = *reinterpret_cast<const uint4*>(ldsb + bcur[m]);
+    for (int tap = 0; tap < 9; tap++) {
+        tap_bases(tap < 8 ? tap + 1 : 8, bnext);
 #pragma unroll
         for (int cc = 0; cc < NCH; cc++) {
             const int ks = tap * NCH + cc;
-            // weights two k-steps ahead (the fragment buffer is padded by two zero k-steps)
-            const uint4 q0 = W[(size_t)(ks + 2) * CF * 64], q1 = W[(size_t)(ks + 2) * CF * 64 + 64];
+            const uint4 a0 = wr[cc % PF][0], a1 = wr[cc % PF][1];
+            // refill this ring slot with k-step ks+PF (of the next layer once past the end)
+            const uint4* Wsrc = (tap == 8 && cc + PF >= NCH) ? Wn : W;
+            wr[cc % PF][0] = Wsrc[(size_t)(ks + PF) * CF * 64];
+            wr[cc % PF][1] = Wsrc[(size_t)(ks + PF) * CF * 64 + 64];
             __builtin_amdgcn_sched_barrier(0);
-            constexpr int LA = 3;
-            uint4 bq[LA];
-#pragma unroll
-            for (int m = 0; m < LA && m < MF; m++) bq[m] = *reinterpret_cast<const uint4*>(ldsb + base[m] + cc * 64);
 #pragma unroll
             for (int m = 0; m < MF; m++) {
                 const uint4 bv = bq[m % LA];
-                if (m + LA < MF) bq[m % LA] = *reinterpret_cast<const uint4*>(ldsb + base[m + LA] + cc * 64);
+                if (m + LA < MF) {
+                    bq[m % LA] = *reinterpret_cast<const uint4*>(ldsb + bcur[m + LA] + cc * 64);
+                } else if (cc + 1 < NCH) {                   // next k-step, same tap
+                    bq[m % LA] = *reinterpret_cast<const uint4*>(ldsb + bcur[m + LA - MF] + (cc + 1) * 64);
+                } else {                                     // first k-step of the next tap
+                    bq[m % LA] = *reinterpret_cast<const uint4*>(ldsb + bnext[m + LA - MF]);
+                }
                 const bf16x8 A0 = __builtin_bit_cast(bf16x8, a0), A1 = __builtin_bit_cast(bf16x8, a1);
                 const bf16x8 Bv = __builtin_bit_cast(bf16x8, bv);
                 acc[m][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A0, Bv, acc[m][0], 0, 0, 0);
                 acc[m][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A1, Bv, acc[m][1], 0, 0, 0);
             }
-            __builtin_amdgcn_sched_group_barrier(0x100, LA < MF ? LA : MF, 0);
 #pragma unroll
             for (int m = 0; m < MF; m++) {
-                if (m + LA < MF) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                 __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
             }
-            a0 = p0; a1 = p1;
-            p0 = q0; p1 = q1;
             __builtin_amdgcn_sched_barrier(0);
         }
+#pragma unroll
+        for (int m = 0; m < MF; m++) bcur[m] = bnext[m];
     }
     (void)KS;
     // `in` and `out` are different buffers, so the epilogue needs no barrier before it;
     // the barrier after it publishes `out` to the next layer.
     char* ob = reinterpret_cast<char*>(out_lds);
+    typedef __attribute__((ext_vector_type(2))) float f32x2;
+    typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+    typedef __attribute__((ext_vector_type(2))) short s16x2;
+    const s16x2 z = {0, 0};
 #pragma unroll
     for (int n = 0; n < 2; n++) {
         const int co = cw * 32 + n * 16 + h * 4;
-        const float4 bb = *reinterpret_cast<const float4*>(bias + co);
+        // per-lane base; each fragment adds a compile-time offset (ds_write immediate)
+        char* lane_base = ob + ((bw * BPW * 64 + (lane & 15)) * RSO + (co >> 3)) * 16 + (co & 7) * 2;
 #pragma unroll
         for (int m = 0; m < MF; m++) {
-            const int b = bw * BPW + (m >> 2);
-            const int sq = (m & 3) * 16 + (lane & 15);
-            bf16x4* dst = reinterpret_cast<bf16x4*>(ob + ((b * 64 + sq) * RSO + (co >> 3)) * 16 + (co & 7) * 2);
-            float v0 = acc[m][n][0] + bb.x, v1 = acc[m][n][1] + bb.y, v2 = acc[m][n][2] + bb.z,
-                  v3 = acc[m][n][3] + bb.w;
+            uint2* dst = reinterpret_cast<uint2*>(lane_base + ((m >> 2) * 64 + (m & 3) * 16) * RSO * 16);
+            f32x2 lo = {acc[m][n][0], acc[m][n][1]}, hi = {acc[m][n][2], acc[m][n][3]};
             if constexpr (RESID) {
-                const bf16x4 r = *dst;
-                v0 += (float)r[0]; v1 += (float)r[1]; v2 += (float)r[2]; v3 += (float)r[3];
+                const uint2 r = *dst;                       // bf16 -> f32 is a 16-bit shift
+                lo += f32x2{__builtin_bit_cast(float, r.x << 16), __builtin_bit_cast(float, r.x & 0xFFFF0000u)};
+                hi += f32x2{__builtin_bit_cast(float, r.y << 16), __builtin_bit_cast(float, r.y & 0xFFFF0000u)};
             }
-            bf16x4 y;
-            y[0] = (__bf16)fmaxf(v0, 0.0f); y[1] = (__bf16)fmaxf(v1, 0.0f);
-            y[2] = (__bf16)fmaxf(v2, 0.0f); y[3] = (__bf16)fmaxf(v3, 0.0f);
-            *dst = y;
+            // round to bf16 (v_cvt_pk_bf16_f32), then ReLU as a signed 16-bit max with 0
+            s16x2 q0 = __builtin_bit_cast(s16x2, __builtin_convertvector(lo, bf16x2));
+            s16x2 q1 = __builtin_bit_cast(s16x2, __builtin_convertvector(hi, bf16x2));
+            q0 = __builtin_elementwise_max(q0, z);
+            q1 = __builtin_elementwise_max(q1, z);
+            *dst = make_uint2(__builtin_bit_cast(unsigned, q0), __builtin_bit_cast(unsigned, q1));
         }
     }
     __syncthreads();
@@ -274,11 +323,20 @@ tower_kernel(const __bf16* __restrict__ planes, TowerArgs ta, const int* __restr
     }
     for (int c = tid; c < ZN; c += NT) lds[2 * XSZ + c] = make_uint4(0, 0, 0, 0);
     __syncthreads();
-    conv_lds<32, RSI, F, RSF, BPW, false>(ldsb, X, XSZ * 16, zero_off, ta.w[0], ta.b[0], cw, bw, lane);
+    {
+        uint4 wr0[RingPF<1>::PF][2];
+        ring_fill<1, F>(wr0, ta.w[0], cw, lane);
+        conv_lds<32, RSI, F, RSF, BPW, false>(ldsb, X, XSZ * 16, zero_off, ta.w[0], nullptr, ta.b[0], wr0, cw, bw,
+                                              lane);
+    }
+    uint4 wr[RingPF<F / 32>::PF][2];
+    if (ta.blocks > 0) ring_fill<F / 32, F>(wr, ta.w[1], cw, lane);
     for (int b = 0; b < ta.blocks; b++) {
-        conv_lds<F, RSF, F, RSF, BPW, false>(ldsb, H, 0, zero_off, ta.w[1 + 2 * b], ta.b[1 + 2 * b], cw, bw, lane);
-        conv_lds<F, RSF, F, RSF, BPW, true>(ldsb, X, XSZ * 16, zero_off, ta.w[2 + 2 * b], ta.b[2 + 2 * b], cw, bw,
-                                            lane);
+        const uint4* after = b + 1 < ta.blocks ? ta.w[3 + 2 * b] : nullptr;
+        conv_lds<F, RSF, F, RSF, BPW, false>(ldsb, H, 0, zero_off, ta.w[1 + 2 * b], ta.w[2 + 2 * b], ta.b[1 + 2 * b],
+                                             wr, cw, bw, lane);
+        conv_lds<F, RSF, F, RSF, BPW, true>(ldsb, X, XSZ * 16, zero_off, ta.w[2 + 2 * b], after, ta.b[2 + 2 * b], wr,
+                                            cw, bw, lane);
     }
     // heads: 256-thread groups, PAR boards at a time, scratch in H
     const int grp = tid >> 8, t = tid & 255;

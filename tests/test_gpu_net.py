@@ -92,5 +92,7 @@ def test_fused_tower_matches_per_layer_kernels(require_gpu, blocks, filters, mon
     monkeypatch.setenv("AZ_FUSED_TOWER", "0")
     layered = A.AlphaZero(blocks, filters, weights=w, dtype="bf16")
     pl, vl = layered.forward(planes)
-    np.testing.assert_allclose(vf, vl, atol=1e-5)
-    np.testing.assert_allclose(pf, pl, rtol=1e-4, atol=1e-8)
+    # same bf16 arithmetic, but the fused path adds the bias before the K sum (accumulator init):
+    # occasional bf16 rounding flips -> bf16-scale tolerance (each path is also checked vs the oracle)
+    np.testing.assert_allclose(vf, vl, atol=2e-3)
+    np.testing.assert_allclose(pf, pl, rtol=2e-2, atol=1e-6)
