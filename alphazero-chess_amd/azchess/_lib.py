@@ -7,7 +7,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libaz.so")
+# AZ_LIB selects an alternative in-tree build of the same ABI (kernel-variant A/B runs)
+LIB_PATH = os.environ.get("AZ_LIB") or os.path.join(_HERE, "libaz.so")
 CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
 
 ACTION_SPACE = 4096

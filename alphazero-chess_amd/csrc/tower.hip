@@ -15,6 +15,12 @@
 
 #include "az_internal.h"
 
+#ifndef AZ_TOWER_WB256
+#define AZ_TOWER_WB256 1   // F=256: 8 waves x 2 boards (WB=2, 16 waves, measured 10% slower: spills)
+#endif
+#ifndef AZ_TOWER_NCO256
+#define AZ_TOWER_NCO256 2
+#endif
 #ifndef AZ_TOWER_PF
 #define AZ_TOWER_PF 2      // weight prefetch depth in k-steps (L2 latency cover; 4 measured no faster)
 #endif
@@ -32,11 +38,13 @@ struct TowerArgs {
     int blocks;
 };
 
+// BPB boards per workgroup; NCO 16-channel output fragments per wave; WB board groups.
+// waves = (F / (16*NCO)) * WB
 template <int F> struct TowerCfg;
-template <> struct TowerCfg<256> { static constexpr int BPB = 2, WB = 1; };
-template <> struct TowerCfg<128> { static constexpr int BPB = 4, WB = 1; };
-template <> struct TowerCfg<64> { static constexpr int BPB = 4, WB = 2; };
-template <> struct TowerCfg<32> { static constexpr int BPB = 8, WB = 4; };
+template <> struct TowerCfg<256> { static constexpr int BPB = 2, WB = AZ_TOWER_WB256, NCO = AZ_TOWER_NCO256; };
+template <> struct TowerCfg<128> { static constexpr int BPB = 4, WB = 1, NCO = 2; };
+template <> struct TowerCfg<64> { static constexpr int BPB = 4, WB = 2, NCO = 2; };
+template <> struct TowerCfg<32> { static constexpr int BPB = 8, WB = 4, NCO = 2; };
 
 __device__ __forceinline__ float t_wave_max(float v) {
     for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
@@ -53,21 +61,23 @@ __device__ __forceinline__ float t_wave_sum(float v) {
 template <int NCH> struct RingPF { static constexpr int PF = NCH >= AZ_TOWER_PF ? AZ_TOWER_PF : NCH; };
 
 // Load k-steps [0, PF) of a layer's weight fragments into the ring.
-template <int NCH, int F>
-__device__ __forceinline__ void ring_fill(uint4 (&wr)[RingPF<NCH>::PF][2], const uint4* __restrict__ wsw, int cw,
+template <int NCH, int F, int NCO>
+__device__ __forceinline__ void ring_fill(uint4 (&wr)[RingPF<NCH>::PF][NCO], const uint4* __restrict__ wsw, int cw,
                                           int lane) {
     constexpr int CF = F / 16;
-    const uint4* W = wsw + (size_t)(cw * 2) * 64 + lane;
+    const uint4* W = wsw + (size_t)(cw * NCO) * 64 + lane;
 #pragma unroll
-    for (int i = 0; i < RingPF<NCH>::PF; i++) { wr[i][0] = W[(size_t)i * CF * 64]; wr[i][1] = W[(size_t)i * CF * 64 + 64]; }
+    for (int i = 0; i < RingPF<NCH>::PF; i++)
+#pragma unroll
+        for (int n = 0; n < NCO; n++) wr[i][n] = W[(size_t)i * CF * 64 + n * 64];
 }
 
 // wr: register ring holding this layer's next PF weight k-steps on entry; on exit it holds
 // the first PF k-steps of `wnext` (the next layer with the same chunk count), or zeros.
-template <int CIN, int RSI, int F, int RSO, int BPW, bool RESID>
+template <int CIN, int RSI, int F, int RSO, int BPW, int NCO, bool RESID>
 __device__ __forceinline__ void conv_lds(const char* __restrict__ ldsb, uint4* __restrict__ out_lds, int in_off,
                                          int zero_off, const uint4* __restrict__ wsw, const uint4* __restrict__ wnext,
-                                         const float* __restrict__ bias, uint4 (&wr)[RingPF<CIN / 32>::PF][2],
+                                         const float* __restrict__ bias, uint4 (&wr)[RingPF<CIN / 32>::PF][NCO],
                                          int cw, int bw, int lane) {
     constexpr int NCH = CIN / 32;                     // 32-channel K chunks (4 slots)
     constexpr int CF = F / 16;
@@ -79,17 +89,16 @@ __device__ __forceinline__ void conv_lds(const char* __restrict__ ldsb, uint4* _
     static_assert(NCH % PF == 0, "prefetch depth must divide the chunk count");
     const int h = lane >> 4;
     // accumulators start at the folded bias: no bias adds in the epilogue
-    const float4 bias0 = *reinterpret_cast<const float4*>(bias + cw * 32 + h * 4);
-    const float4 bias1 = *reinterpret_cast<const float4*>(bias + cw * 32 + 16 + h * 4);
-    f32x4 acc[MF][2];
+    f32x4 acc[MF][NCO];
 #pragma unroll
-    for (int m = 0; m < MF; m++) {
-        acc[m][0] = f32x4{bias0.x, bias0.y, bias0.z, bias0.w};
-        acc[m][1] = f32x4{bias1.x, bias1.y, bias1.z, bias1.w};
+    for (int n = 0; n < NCO; n++) {
+        const float4 bn = *reinterpret_cast<const float4*>(bias + cw * 16 * NCO + n * 16 + h * 4);
+#pragma unroll
+        for (int m = 0; m < MF; m++) acc[m][n] = f32x4{bn.x, bn.y, bn.z, bn.w};
     }
-    const uint4* W = wsw + (size_t)(cw * 2) * 64 + lane;
+    const uint4* W = wsw + (size_t)(cw * NCO) * 64 + lane;
     // past the last k-step the refills read the next layer (or this layer's zero padding)
-    const uint4* Wn = (wnext ? wnext + (size_t)(cw * 2) * 64 + lane : W + (size_t)KS * CF * 64) - (size_t)KS * CF * 64;
+    const uint4* Wn = (wnext ? wnext + (size_t)(cw * NCO) * 64 + lane : W + (size_t)KS * CF * 64) - (size_t)KS * CF * 64;
     // B-fragment (activation) reads run LA fragments ahead, across k-step and tap boundaries:
     // the first LA reads of step s+1 are issued inside step s.
     constexpr int LA = 4;
@@ -116,11 +125,13 @@ __device__ __forceinline__ void conv_lds(const char* __restrict__ ldsb, uint4* _
 #pragma unroll
         for (int cc = 0; cc < NCH; cc++) {
             const int ks = tap * NCH + cc;
-            const uint4 a0 = wr[cc % PF][0], a1 = wr[cc % PF][1];
+            uint4 a[NCO];
+#pragma unroll
+            for (int n = 0; n < NCO; n++) a[n] = wr[cc % PF][n];
             // refill this ring slot with k-step ks+PF (of the next layer once past the end)
             const uint4* Wsrc = (tap == 8 && cc + PF >= NCH) ? Wn : W;
-            wr[cc % PF][0] = Wsrc[(size_t)(ks + PF) * CF * 64];
-            wr[cc % PF][1] = Wsrc[(size_t)(ks + PF) * CF * 64 + 64];
+#pragma unroll
+            for (int n = 0; n < NCO; n++) wr[cc % PF][n] = Wsrc[(size_t)(ks + PF) * CF * 64 + n * 64];
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int m = 0; m < MF; m++) {
@@ -132,15 +143,16 @@ __device__ __forceinline__ void conv_lds(const char* __restrict__ ldsb, uint4* _
                 } else {                                     // first k-step of the next tap
                     bq[m % LA] = *reinterpret_cast<const uint4*>(ldsb + bnext[m + LA - MF]);
                 }
-                const bf16x8 A0 = __builtin_bit_cast(bf16x8, a0), A1 = __builtin_bit_cast(bf16x8, a1);
                 const bf16x8 Bv = __builtin_bit_cast(bf16x8, bv);
-                acc[m][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A0, Bv, acc[m][0], 0, 0, 0);
-                acc[m][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A1, Bv, acc[m][1], 0, 0, 0);
+#pragma unroll
+                for (int n = 0; n < NCO; n++)
+                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[n]), Bv,
+                                                                        acc[m][n], 0, 0, 0);
             }
 #pragma unroll
             for (int m = 0; m < MF; m++) {
                 __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, NCO, 0);
             }
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -156,8 +168,8 @@ __device__ __forceinline__ void conv_lds(const char* __restrict__ ldsb, uint4* _
     typedef __attribute__((ext_vector_type(2))) short s16x2;
     const s16x2 z = {0, 0};
 #pragma unroll
-    for (int n = 0; n < 2; n++) {
-        const int co = cw * 32 + n * 16 + h * 4;
+    for (int n = 0; n < NCO; n++) {
+        const int co = cw * 16 * NCO + n * 16 + h * 4;
         // per-lane base; each fragment adds a compile-time offset (ds_write immediate)
         char* lane_base = ob + ((bw * BPW * 64 + (lane & 15)) * RSO + (co >> 3)) * 16 + (co & 7) * 2;
 #pragma unroll
@@ -183,8 +195,9 @@ __device__ __forceinline__ void conv_lds(const char* __restrict__ ldsb, uint4* _
 // heads for one board from the LDS image x (bf16, row stride RS slots); 256 threads (t < 256).
 template <int F, int RS, bool SEARCH>
 __device__ __forceinline__ void heads_lds(const char* __restrict__ xb, float* __restrict__ scratch, int t,
-                                          const float* __restrict__ head, bool valid, int row, float* pol_out,
-                                          float* val_out, const SearchOut& so) {
+                                          const float* __restrict__ head, bool writer, bool valid, int row,
+                                          float* pol_out, float* val_out, const SearchOut& so) {
+    // writer: this 256-thread group owns `scratch` (idle groups only join the barriers)
     const HeadLayout L = HeadLayout::make(F);
     float* p1 = scratch;                 // [32][64]
     float* v1 = p1 + 32 * 64;            // [8][64]
@@ -233,7 +246,7 @@ __device__ __forceinline__ void heads_lds(const char* __restrict__ xb, float* __
         red[g * 64 + o] = a;
     }
     mx = t_wave_max(mx);
-    if ((t & 63) == 0) stat[g] = mx;
+    if (writer && (t & 63) == 0) stat[g] = mx;
     __syncthreads();
     mx = fmaxf(fmaxf(stat[0], stat[1]), fmaxf(stat[2], stat[3]));
     float s = 0.0f;
@@ -241,13 +254,13 @@ __device__ __forceinline__ void heads_lds(const char* __restrict__ xb, float* __
         for (int i = t; i < 4096; i += 256) s += expf(lg[i] - mx);
     s = t_wave_sum(s);
     float hv = 0.0f;
-    if (t < 64) {
+    if (writer && t < 64) {
         const float hsum = red[t] + red[64 + t] + red[128 + t] + red[192 + t] + head[L.l1b + t];
         hv = fmaxf(hsum, 0.0f) * head[L.l2w + t];
     }
     __syncthreads();
-    if ((t & 63) == 0) stat[4 + g] = s;
-    if (t < 64) {
+    if (writer && (t & 63) == 0) stat[4 + g] = s;
+    if (writer && t < 64) {
         hv = t_wave_sum(hv);
         if (t == 0) red[0] = tanhf(hv + head[L.l2b]);
     }
@@ -289,17 +302,17 @@ __device__ __forceinline__ void heads_lds(const char* __restrict__ xb, float* __
 }
 
 template <int F, bool SEARCH>
-__global__ void __launch_bounds__((F / 32) * TowerCfg<F>::WB * 64)
+__global__ void __launch_bounds__((F / (16 * TowerCfg<F>::NCO)) * TowerCfg<F>::WB * 64)
 tower_kernel(const __bf16* __restrict__ planes, TowerArgs ta, const int* __restrict__ count_ptr, int rows,
              float* __restrict__ pol_out, float* __restrict__ val_out, SearchOut so) {
-    constexpr int BPB = TowerCfg<F>::BPB, WB = TowerCfg<F>::WB, BPW = BPB / WB;
-    constexpr int NCW = F / 32;
+    constexpr int BPB = TowerCfg<F>::BPB, WB = TowerCfg<F>::WB, BPW = BPB / WB, NCO = TowerCfg<F>::NCO;
+    constexpr int NCW = F / (16 * NCO);
     constexpr int NT = NCW * WB * 64;
     constexpr int RSF = F / 8 + 2, RSI = 32 / 8 + 2;
     constexpr int XSZ = BPB * 64 * RSF;               // slots per activation buffer
     constexpr int ZN = 16 + F / 8;
     constexpr int HEADS_FLOATS = 32 * 64 + 8 * 64 + 4096 + 256 + 16;
-    constexpr int PAR = NT / 256;                      // boards whose heads run concurrently
+    constexpr int PAR = NT / 256 < BPB ? NT / 256 : BPB;   // boards whose heads run concurrently
     static_assert(NT % 256 == 0, "heads need 256-thread groups");
     static_assert(PAR * HEADS_FLOATS * 4 <= XSZ * 16, "heads scratch must fit in h");
     __shared__ __attribute__((aligned(16))) uint4 lds[2 * XSZ + ZN];
@@ -324,28 +337,28 @@ tower_kernel(const __bf16* __restrict__ planes, TowerArgs ta, const int* __restr
     for (int c = tid; c < ZN; c += NT) lds[2 * XSZ + c] = make_uint4(0, 0, 0, 0);
     __syncthreads();
     {
-        uint4 wr0[RingPF<1>::PF][2];
-        ring_fill<1, F>(wr0, ta.w[0], cw, lane);
-        conv_lds<32, RSI, F, RSF, BPW, false>(ldsb, X, XSZ * 16, zero_off, ta.w[0], nullptr, ta.b[0], wr0, cw, bw,
-                                              lane);
+        uint4 wr0[RingPF<1>::PF][NCO];
+        ring_fill<1, F, NCO>(wr0, ta.w[0], cw, lane);
+        conv_lds<32, RSI, F, RSF, BPW, NCO, false>(ldsb, X, XSZ * 16, zero_off, ta.w[0], nullptr, ta.b[0], wr0, cw,
+                                                   bw, lane);
     }
-    uint4 wr[RingPF<F / 32>::PF][2];
-    if (ta.blocks > 0) ring_fill<F / 32, F>(wr, ta.w[1], cw, lane);
+    uint4 wr[RingPF<F / 32>::PF][NCO];
+    if (ta.blocks > 0) ring_fill<F / 32, F, NCO>(wr, ta.w[1], cw, lane);
     for (int b = 0; b < ta.blocks; b++) {
         const uint4* after = b + 1 < ta.blocks ? ta.w[3 + 2 * b] : nullptr;
-        conv_lds<F, RSF, F, RSF, BPW, false>(ldsb, H, 0, zero_off, ta.w[1 + 2 * b], ta.w[2 + 2 * b], ta.b[1 + 2 * b],
-                                             wr, cw, bw, lane);
-        conv_lds<F, RSF, F, RSF, BPW, true>(ldsb, X, XSZ * 16, zero_off, ta.w[2 + 2 * b], after, ta.b[2 + 2 * b], wr,
-                                            cw, bw, lane);
+        conv_lds<F, RSF, F, RSF, BPW, NCO, false>(ldsb, H, 0, zero_off, ta.w[1 + 2 * b], ta.w[2 + 2 * b],
+                                                  ta.b[1 + 2 * b], wr, cw, bw, lane);
+        conv_lds<F, RSF, F, RSF, BPW, NCO, true>(ldsb, X, XSZ * 16, zero_off, ta.w[2 + 2 * b], after, ta.b[2 + 2 * b],
+                                                 wr, cw, bw, lane);
     }
     // heads: 256-thread groups, PAR boards at a time, scratch in H
     const int grp = tid >> 8, t = tid & 255;
-    float* scratch = reinterpret_cast<float*>(H) + grp * HEADS_FLOATS;
+    float* scratch = reinterpret_cast<float*>(H) + (grp < PAR ? grp : 0) * HEADS_FLOATS;
     for (int b0 = 0; b0 < BPB; b0 += PAR) {
         const int b = b0 + grp;
-        const bool valid = b < nb;
-        heads_lds<F, RSF, SEARCH>(ldsb + (size_t)b * 64 * RSF * 16, scratch, t, ta.head, valid, row0 + b, pol_out,
-                                  val_out, so);
+        const bool valid = grp < PAR && b < nb;
+        heads_lds<F, RSF, SEARCH>(ldsb + (size_t)(b < BPB ? b : 0) * 64 * RSF * 16, scratch, t, ta.head, grp < PAR,
+                                  valid, row0 + b, pol_out, val_out, so);
         __syncthreads();
         if constexpr (SEARCH) {
             if (valid && so.log_cap > 0) {
@@ -388,7 +401,7 @@ int tower_forward(NetDev* n, const void* planes, const int* count, int rows, flo
 #define AZ_TOWER(FF)                                                                                           \
     if (n->filters == FF) {                                                                                    \
         constexpr int BPB = TowerCfg<FF>::BPB;                                                                 \
-        constexpr int NT = (FF / 32) * TowerCfg<FF>::WB * 64;                                                  \
+        constexpr int NT = (FF / (16 * TowerCfg<FF>::NCO)) * TowerCfg<FF>::WB * 64;                            \
         const int grid = (rows + BPB - 1) / BPB;                                                               \
         if (so) tower_kernel<FF, true><<<grid, NT, 0, st>>>((const __bf16*)planes, ta, count, rows, pol, val, s); \
         else tower_kernel<FF, false><<<grid, NT, 0, st>>>((const __bf16*)planes, ta, count, rows, pol, val, s);  \

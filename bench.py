@@ -70,6 +70,12 @@ def main():
     import azchess as A
     from azchess.dist import barrier as dist_barrier, env_rank, reduce_run, shard
     rank, world, local = env_rank()
+    import ctypes
+    ndev = ctypes.c_int(0)
+    A._lib.lib.az_device_count(ctypes.byref(ndev))
+    if ndev.value < 1:
+        raise SystemExit("bench.py: no GPU visible to libaz")
+    local = local % ndev.value          # one GPU per rank; wraps only when rehearsing on fewer GPUs
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")
