@@ -26,6 +26,19 @@ sys.path.insert(0, os.path.join(ROOT, "alphazero-chess_amd"))
 PEAK_BF16_TFLOPS = 2500.0     # MI355X_MICROARCH.md: ~2.5 PF dense bf16
 PEAK_F32_TFLOPS = 157.3       # MI355X_MICROARCH.md: f32 MFMA = vector peak
 PEAK_HBM_GBS = 8000.0         # MI355X_MICROARCH.md: 8.0 TB/s spec
+# HBM bytes per tower launch from rocprofv3 PMC passes (tools/pmc_run.sh: FETCH_SIZE x2 per the
+# gfx950 correction + WRITE_SIZE), same kernel and per-launch work (2048 rows, 20x256 bf16)
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_tower_summary.json")
+
+
+def pmc_traffic(games, blocks, filters, dtype):
+    """Per-launch HBM traffic of the dominant kernel from the committed PMC summary, or None
+    when the bench workload is not the one the counters were collected on."""
+    if (games, blocks, filters, dtype) != (2048, 20, 256, "bf16") or not os.path.exists(PMC_SUMMARY):
+        return None, None
+    with open(PMC_SUMMARY) as f:
+        s = json.load(f)
+    return s.get("traffic_bytes"), os.path.relpath(PMC_SUMMARY, ROOT)
 
 
 def cpu_baseline(blocks, filters, threads, games, sims):
@@ -135,6 +148,7 @@ def main():
         dist.destroy_process_group()
         return
     value = sims_all / elapsed
+    traffic, traffic_src = pmc_traffic(G, args.blocks, args.filters, args.dtype)
     peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
     conv_tflops = tm["conv_flop"] / (tm["conv_ms"] * 1e-3) / 1e12 if tm["conv_ms"] > 0 else 0.0
     tower_tflops = tm["tower_flop"] / (tm["tower_ms"] * 1e-3) / 1e12 if tm["tower_ms"] > 0 else 0.0
@@ -159,7 +173,8 @@ def main():
                    "fen_cache": "off for value (see with_fen_cache)",
                    "parallelism": "games sharded %d-way, no collective (gloo barrier/max only)" % world},
         "roofline": {"bound": "mfma", "achieved": conv_tflops, "peak": peak, "unit": "TFLOP/s",
-                     "frac": conv_tflops / peak, "traffic": None,
+                     "frac": conv_tflops / peak, "traffic": traffic,
+                     "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
                      "kernel": ("tower_kernel<%d> (fused input conv + %d residual convs + heads; algorithmic "
                                 "FLOPs = conv FLOPs only), %d launches timed" % (args.filters, 2 * args.blocks,
                                                                                  tm["conv_launches"]))
