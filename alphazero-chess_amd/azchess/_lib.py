@@ -97,6 +97,20 @@ SIGNATURES = [
     ("az_search_eval_log", C.c_int, [C.c_void_p, P(C.c_int64), P(C.c_int64), P(C.c_uint64), P(C.c_float),
                                      P(C.c_int32), P(C.c_int32), P(C.c_float)]),
     ("az_search_timing", C.c_int, [C.c_void_p, P(AzTiming), C.c_int, C.c_int]),
+    ("az_cyclical_lr", C.c_double, [C.c_int]),
+    ("az_trainer_create", C.c_int, [C.c_int, C.c_int, P(C.c_float), C.c_size_t, C.c_int, C.c_int,
+                                    P(C.c_void_p)]),
+    ("az_trainer_destroy", C.c_int, [C.c_void_p]),
+    ("az_trainer_compute_grads", C.c_int, [C.c_void_p, P(C.c_float), P(C.c_float), P(C.c_float), C.c_int,
+                                           P(C.c_float)]),
+    ("az_trainer_apply", C.c_int, [C.c_void_p, C.c_double]),
+    ("az_trainer_step", C.c_int, [C.c_void_p, P(C.c_float), P(C.c_float), P(C.c_float), C.c_int, C.c_double,
+                                  P(C.c_float)]),
+    ("az_trainer_get_params", C.c_int, [C.c_void_p, P(C.c_float), C.c_size_t]),
+    ("az_trainer_get_grads", C.c_int, [C.c_void_p, P(C.c_float), C.c_size_t]),
+    ("az_trainer_relu_output", C.c_int, [C.c_void_p, C.c_int, P(C.c_float), C.c_size_t]),
+    ("az_comm_unique_id", C.c_int, [C.c_void_p, C.c_int]),
+    ("az_trainer_set_comm", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int]),
 ]
 
 if not os.path.exists(LIB_PATH):

@@ -92,3 +92,104 @@ def process_batch(states, model):
     """training.rs:380-422: one batched forward over the requests' positions."""
     x = np.concatenate([to_tensor(s) for s in states], 0)
     return model.forward(x)
+
+
+# ---------------------------------------------------------------- train() (SURVEY 8f row 1)
+def get_cyclical_lr(iteration):
+    """training.rs:424-441"""
+    return float(L.lib.az_cyclical_lr(int(iteration)))
+
+
+def comm_unique_id():
+    """RCCL unique id (128 bytes) for Trainer.set_comm; create on rank 0, share over the host."""
+    buf = (C.c_char * 128)()
+    L.check(L.lib.az_comm_unique_id(buf, 128))
+    return bytes(buf)
+
+
+class Trainer:
+    """The reference's training half of train() (training.rs:137-190) on one GPU: the model's
+    flat parameters, the AdamW state (training.rs:63-66) and every activation of a batch live
+    in HBM; one step = forward in training mode + compute_gradients + optimizer.step.
+    Data-parallel over RCCL with set_comm (gradients summed over ranks before clipping)."""
+
+    def __init__(self, blocks, filters, weights=None, max_batch=512, device=0, seed=42):
+        from .agent import random_weights
+        if weights is None:
+            weights = random_weights(blocks, filters, seed)
+        self.blocks, self.filters, self.device = blocks, filters, device
+        self.n = int(L.lib.az_net_num_params(blocks, filters))
+        w = np.ascontiguousarray(weights, np.float32)
+        h = C.c_void_p()
+        L.check(L.lib.az_trainer_create(blocks, filters, L.fptr(w), w.size, max_batch, device, C.byref(h)))
+        self._h = h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            L.lib.az_trainer_destroy(h)
+            self._h = None
+
+    @staticmethod
+    def _batch(planes, tpol, tval):
+        planes = np.ascontiguousarray(planes, np.float32).reshape(-1, 19 * 64)
+        tpol = np.ascontiguousarray(tpol, np.float32).reshape(-1, 4096)
+        tval = np.ascontiguousarray(tval, np.float32).reshape(-1)
+        assert planes.shape[0] == tpol.shape[0] == tval.shape[0]
+        return planes, tpol, tval
+
+    def compute_gradients(self, planes, tpol, tval):
+        planes, tpol, tval = self._batch(planes, tpol, tval)
+        loss = np.zeros(2, np.float32)
+        L.check(L.lib.az_trainer_compute_grads(self._h, L.fptr(planes), L.fptr(tpol), L.fptr(tval),
+                                               planes.shape[0], L.fptr(loss)))
+        return float(loss[0]), float(loss[1])
+
+    def apply(self, lr):
+        L.check(L.lib.az_trainer_apply(self._h, float(lr)))
+
+    def step(self, planes, tpol, tval, lr):
+        planes, tpol, tval = self._batch(planes, tpol, tval)
+        loss = np.zeros(2, np.float32)
+        L.check(L.lib.az_trainer_step(self._h, L.fptr(planes), L.fptr(tpol), L.fptr(tval), planes.shape[0],
+                                      float(lr), L.fptr(loss)))
+        return float(loss[0]), float(loss[1])
+
+    def params(self):
+        out = np.empty(self.n, np.float32)
+        L.check(L.lib.az_trainer_get_params(self._h, L.fptr(out), self.n))
+        return out
+
+    def grads(self):
+        out = np.empty(self.n, np.float32)
+        L.check(L.lib.az_trainer_get_grads(self._h, L.fptr(out), self.n))
+        return out
+
+    def relu_masks(self, batch):
+        """ReLU masks of the last forward in forward order (parity tests): tower layers as
+        NCHW [B, F, 8, 8], heads [B, 40, 8, 8], value hidden [B, 64]."""
+        out, F = [], self.filters
+        for layer in range(2 * self.blocks + 3):
+            if layer <= 2 * self.blocks:
+                a = np.empty(batch * 64 * F, np.float32)
+            elif layer == 2 * self.blocks + 1:
+                a = np.empty(batch * 64 * 64, np.float32)
+            else:
+                a = np.empty(batch * 64, np.float32)
+            L.check(L.lib.az_trainer_relu_output(self._h, layer, L.fptr(a), a.size))
+            if layer <= 2 * self.blocks:
+                out.append(a.reshape(batch, 8, 8, F).transpose(0, 3, 1, 2) > 0)
+            elif layer == 2 * self.blocks + 1:
+                out.append(a.reshape(batch, 8, 8, 64).transpose(0, 3, 1, 2)[:, :40] > 0)
+            else:
+                out.append(a.reshape(batch, 64) > 0)
+        return out
+
+    def set_comm(self, unique_id, rank, world):
+        buf = (C.c_char * 128).from_buffer_copy(unique_id)
+        L.check(L.lib.az_trainer_set_comm(self._h, buf, int(rank), int(world)))
+
+    def model(self, dtype="bf16"):
+        """model.valid() for self-play (training.rs:83): an inference net with the current weights."""
+        from .agent import AlphaZero
+        return AlphaZero(self.blocks, self.filters, weights=self.params(), dtype=dtype, device=self.device)

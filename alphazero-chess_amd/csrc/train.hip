@@ -1,0 +1,983 @@
+// train.hip -- the training step of training.rs:137-200 / 277-292 on gfx950, f32 end to end
+// (the reference trains in f32: burn 0.18 CUDA backend, FullPrecisionSettings records).
+//
+// Activations are NHWC f32 [row = board*64 + square][channels].  Every convolution is an
+// implicit GEMM on v_mfma_f32_16x16x4_f32 (exact f32 FMA chains -- the reference's precision):
+//   forward      Y[r][n]      = b[n] + sum_t sum_k X[r + d_t][k] * Wf[t][k][n]
+//   data grad    dX[r][k]     =        sum_t sum_n dY[r + d_t][n] * Wd[t][n][k],  Wd[t] = Wf[8-t]^T
+//   weight grad  dWf[t][k][n] = sum_r X[r + d_t][k] * dY[r][n]    (row splits, fixed-order reduce)
+// where d_t is the 3x3 tap shift inside the 8x8 board with zero padding (agent.rs:21-23,
+// PaddingConfig2d::Same); the 1x1 head convs and the Linear layers are the TAPS = 1 case over
+// generic rows.  BatchNorm runs in training mode (batch statistics, biased variance, running
+// statistics updated with momentum 0.1 -- burn BatchNorm::forward_train, restated), then ReLU /
+// residual; the loss is training.rs:277-292 (policy CE with log(p + 1e-5), 0.5 * MSE value);
+// gradients are clipped by value to [-1, 1] and applied with burn's AdamW (training.rs:63-66:
+// beta 0.9 / 0.999, eps 1e-5 outside the sqrt, decoupled weight decay 1e-4).
+// Every reduction has a fixed order, so a step is bit-reproducible run to run.
+// Data-parallel (training.rs:137-190 on N GPUs): the flat gradient is summed over
+// ranks with ncclAllReduce (RCCL over xGMI) on the trainer's stream before clipping; BatchNorm
+// running statistics are averaged the same way after the step.
+#include <math.h>
+#include <string.h>
+
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "az_internal.h"
+
+namespace azi {
+namespace tr {
+
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+// source row of tap t for row r (board-major rows); false = zero padding
+__device__ __forceinline__ bool tap_src(int r, int t, int& src) {
+    const int sq = r & 63, rr = (sq >> 3) + t / 3 - 1, ff = (sq & 7) + t % 3 - 1;
+    src = (r & ~63) + rr * 8 + ff;
+    return (unsigned)rr < 8u && (unsigned)ff < 8u;
+}
+
+// ------------------------------------------------------------------ forward / data-grad GEMM
+// Tile: 128 rows x 64 columns per 256-thread workgroup (4 waves, 2 x 2: 64 rows x 32 columns per
+// wave = 4 x 2 accumulators of 16x16), K staged 16 channels at a time (all TAPS weight slices of
+// the chunk in LDS).  Requires K % 16 == 0, N % 16 == 0, ldx/ldy % 4 == 0, and R % 64 == 0 when
+// TAPS == 9 (whole boards).
+constexpr int CM = 128, CN = 64, CK = 16;
+constexpr int XS = CK + 1;     // A-tile row stride (floats): 16 consecutive rows hit 16 banks
+constexpr int WS = CN + 16;    // B-tile row stride: rows k and k+1 land on disjoint bank halves
+
+template <int TAPS>
+__global__ void __launch_bounds__(256)
+conv_f32_kernel(const float* __restrict__ X, int ldx, int K, const float* __restrict__ W, int N,
+                const float* __restrict__ bias, const float* __restrict__ addend, float* __restrict__ Y, int ldy,
+                int R) {
+    __shared__ float xs[CM * XS + XS];    // + one zero row read by off-board taps
+    __shared__ __attribute__((aligned(16))) float ws[TAPS * CK * WS];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w & 1, wn = w >> 1;
+    const int r0 = blockIdx.x * CM, n0 = blockIdx.y * CN;
+    f32x4 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; i++) acc[i][0] = acc[i][1] = f32x4{0, 0, 0, 0};
+    if (tid < XS) xs[CM * XS + tid] = 0.0f;
+    for (int k0 = 0; k0 < K; k0 += CK) {
+        __syncthreads();
+        for (int i = tid; i < CM * (CK / 4); i += 256) {
+            const int rr = i >> 2, c4 = (i & 3) * 4;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (r0 + rr < R) v = *reinterpret_cast<const float4*>(X + (size_t)(r0 + rr) * ldx + k0 + c4);
+            float* d = xs + rr * XS + c4;
+            d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+        }
+        for (int i = tid; i < TAPS * CK * (CN / 4); i += 256) {
+            const int t = i / (CK * CN / 4), rem = i % (CK * CN / 4), kk = rem / (CN / 4), n4 = (rem % (CN / 4)) * 4;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (n0 + n4 < N) v = *reinterpret_cast<const float4*>(W + ((size_t)t * K + k0 + kk) * N + n0 + n4);
+            *reinterpret_cast<float4*>(ws + (t * CK + kk) * WS + n4) = v;
+        }
+        __syncthreads();
+#pragma unroll 1
+        for (int t = 0; t < TAPS; t++) {
+            int aoff[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int row = wm * 64 + i * 16 + (lane & 15);
+                if constexpr (TAPS == 9) {
+                    int src;
+                    const bool ok = tap_src(r0 + row, t, src);
+                    aoff[i] = ok ? (src - r0) * XS : CM * XS;
+                } else {
+                    aoff[i] = row * XS;
+                }
+            }
+#pragma unroll
+            for (int kk4 = 0; kk4 < CK / 4; kk4++) {
+                const int kq = kk4 * 4 + (lane >> 4);
+                float a[4], b[2];
+#pragma unroll
+                for (int i = 0; i < 4; i++) a[i] = xs[aoff[i] + kq];
+#pragma unroll
+                for (int j = 0; j < 2; j++) b[j] = ws[(t * CK + kq) * WS + wn * 32 + j * 16 + (lane & 15)];
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+#pragma unroll
+                    for (int j = 0; j < 2; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        const int col = n0 + wn * 32 + j * 16 + (lane & 15);
+        if (col >= N) continue;
+        const float bc = bias ? bias[col] : 0.0f;
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                const int row = r0 + wm * 64 + i * 16 + (lane >> 4) * 4 + g;
+                if (row >= R) continue;
+                float v = acc[i][j][g];
+                if (bias) v += bc;
+                if (addend) v += addend[(size_t)row * ldy + col];
+                Y[(size_t)row * ldy + col] = v;
+            }
+    }
+}
+
+// ------------------------------------------------------------------ weight-grad GEMM
+// Tile: 64 k x 64 n, all TAPS, rows consumed 64 at a time (one board when TAPS == 9) inside the
+// workgroup's row split; wave w owns columns [16w, 16w+16): TAPS x 4 accumulators.
+// partial[split][t][k][n]; reduced over splits in a fixed order by reduce_kernel.
+constexpr int GK = 64, GN = 64, GR = 64, GS = 80;
+
+template <int TAPS>
+__global__ void __launch_bounds__(256)
+wgrad_f32_kernel(const float* __restrict__ X, int ldx, int K, const float* __restrict__ DY, int ldd, int N, int R,
+                 int rows_per_split, float* __restrict__ partial) {
+    __shared__ __attribute__((aligned(16))) float xs[GR * GS + GS];
+    __shared__ __attribute__((aligned(16))) float ds[GR * GS];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int k0 = blockIdx.x * GK, n0 = blockIdx.y * GN, split = blockIdx.z;
+    const int rbeg = split * rows_per_split, rend = min(R, rbeg + rows_per_split);
+    f32x4 acc[TAPS][4];
+#pragma unroll
+    for (int t = 0; t < TAPS; t++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) acc[t][i] = f32x4{0, 0, 0, 0};
+    if (tid < GS) xs[GR * GS + tid] = 0.0f;
+    for (int rc = rbeg; rc < rend; rc += GR) {
+        __syncthreads();
+        for (int i = tid; i < GR * 16; i += 256) {
+            const int rr = i >> 4, c4 = (i & 15) * 4;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f), d = v;
+            if (rc + rr < rend) {
+                if (k0 + c4 < K) v = *reinterpret_cast<const float4*>(X + (size_t)(rc + rr) * ldx + k0 + c4);
+                if (n0 + c4 < N) d = *reinterpret_cast<const float4*>(DY + (size_t)(rc + rr) * ldd + n0 + c4);
+            }
+            *reinterpret_cast<float4*>(xs + rr * GS + c4) = v;
+            *reinterpret_cast<float4*>(ds + rr * GS + c4) = d;
+        }
+        __syncthreads();
+#pragma unroll 2
+        for (int q = 0; q < GR / 4; q++) {
+            const int rq = q * 4 + (lane >> 4);
+            const float b = ds[rq * GS + w * 16 + (lane & 15)];
+#pragma unroll
+            for (int t = 0; t < TAPS; t++) {
+                int src = rq;
+                bool ok = true;
+                if constexpr (TAPS == 9) ok = tap_src(rq, t, src);
+                const int base = ok ? src * GS : GR * GS;
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+                    acc[t][i] = __builtin_amdgcn_mfma_f32_16x16x4f32(xs[base + i * 16 + (lane & 15)], b, acc[t][i], 0, 0, 0);
+            }
+        }
+    }
+    const int n = n0 + w * 16 + (lane & 15);
+    if (n >= N) return;
+#pragma unroll
+    for (int t = 0; t < TAPS; t++)
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                const int kd = k0 + i * 16 + (lane >> 4) * 4 + g;
+                if (kd < K) partial[(((size_t)split * TAPS + t) * K + kd) * N + n] = acc[t][i][g];
+            }
+}
+
+// out[e] = sum over splits s (in order) of partial[s][e]
+__global__ void reduce_kernel(const float* __restrict__ partial, int splits, size_t n, float* __restrict__ out) {
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
+        float s = 0.0f;
+        for (int k = 0; k < splits; k++) s += partial[(size_t)k * n + e];
+        out[e] = s;
+    }
+}
+
+// ------------------------------------------------------------------ column reductions
+// Per-channel sums over rows, fixed order: block (x = row block, y = 64-channel block); thread
+// (phase p = tid/64, channel c) sums rows rbeg+p, rbeg+p+4, ...; phases are combined in order.
+//   MODE 0: sum v                       (bias grads, BN mean)
+//   MODE 1: sum (v - mean)^2            (BN biased variance, two-pass like burn)
+//   MODE 2: sum dz, sum dz*yhat with dz = dout*(o > 0), yhat = (y - mean)/std   (BN backward)
+constexpr int CS_ROWS = 256;   // rows per block
+
+template <int MODE>
+__global__ void __launch_bounds__(256)
+colsum_kernel(const float* __restrict__ V, int ld, int C, int R, const float* __restrict__ mean,
+              const float* __restrict__ stdv, const float* __restrict__ O, const float* __restrict__ Y,
+              float* __restrict__ part) {
+    __shared__ float sh[2][4][64];
+    const int tid = threadIdx.x, p = tid >> 6, c = blockIdx.y * 64 + (tid & 63);
+    const int rbeg = blockIdx.x * CS_ROWS, rend = min(R, rbeg + CS_ROWS);
+    float s0 = 0.0f, s1 = 0.0f;
+    if (c < C) {
+        const float mu = (MODE >= 1) ? mean[c] : 0.0f;
+        const float sd = (MODE == 2) ? stdv[c] : 1.0f;
+        for (int r = rbeg + p; r < rend; r += 4) {
+            const size_t e = (size_t)r * ld + c;
+            if constexpr (MODE == 0) {
+                s0 += V[e];
+            } else if constexpr (MODE == 1) {
+                const float d = V[e] - mu;
+                s0 += d * d;
+            } else {
+                const float dz = O[e] > 0.0f ? V[e] : 0.0f;
+                s0 += dz;
+                s1 += dz * ((Y[e] - mu) / sd);
+            }
+        }
+    }
+    sh[0][p][tid & 63] = s0;
+    sh[1][p][tid & 63] = s1;
+    __syncthreads();
+    if (p == 0 && c < C) {
+        const float a = ((sh[0][0][tid] + sh[0][1][tid]) + sh[0][2][tid]) + sh[0][3][tid];
+        part[((size_t)blockIdx.x * 2 + 0) * C + c] = a;
+        if (MODE == 2) part[((size_t)blockIdx.x * 2 + 1) * C + c] = ((sh[1][0][tid] + sh[1][1][tid]) + sh[1][2][tid]) + sh[1][3][tid];
+    }
+}
+
+// sum the row-block partials of channel c in order
+__device__ __forceinline__ float part_sum(const float* part, int nblk, int C, int c, int which) {
+    float s = 0.0f;
+    for (int b = 0; b < nblk; b++) s += part[((size_t)b * 2 + which) * C + c];
+    return s;
+}
+
+// dst[c] = sum  (bias gradients)
+__global__ void finalize_sum_kernel(const float* __restrict__ part, int nblk, int C, float* __restrict__ dst) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c < C) dst[c] = part_sum(part, nblk, C, c, 0);
+}
+
+// mean[c] = sum / R
+__global__ void finalize_mean_kernel(const float* __restrict__ part, int nblk, int C, int R, float* __restrict__ mean) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c < C) mean[c] = part_sum(part, nblk, C, c, 0) / (float)R;
+}
+
+// var = sum / R; std = sqrt(var + eps); running stats: rm = rm*0.9 + mean*0.1, rv = rv*0.9 + var*0.1
+__global__ void finalize_var_kernel(const float* __restrict__ part, int nblk, int C, int R, const float* __restrict__ mean,
+                                    float* __restrict__ stdv, float* __restrict__ rmean, float* __restrict__ rvar) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const float var = part_sum(part, nblk, C, c, 0) / (float)R;
+    stdv[c] = sqrtf(var + 1e-5f);
+    rmean[c] = rmean[c] * 0.9f + mean[c] * 0.1f;
+    rvar[c] = rvar[c] * 0.9f + var * 0.1f;
+}
+
+// BN backward sums: dbeta[c] = sum dz, dgamma[c] = sum dz*yhat
+__global__ void finalize_bnback_kernel(const float* __restrict__ part, int nblk, int C, float* __restrict__ dgamma,
+                                       float* __restrict__ dbeta) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    dbeta[c] = part_sum(part, nblk, C, c, 0);
+    dgamma[c] = part_sum(part, nblk, C, c, 1);
+}
+
+// ------------------------------------------------------------------ element-wise
+// out = relu(((y - mean) / std) * gamma + beta [+ res])   (burn BatchNorm::forward_shared + relu)
+__global__ void bn_apply_kernel(const float* __restrict__ Y, int ld, int C, int R, const float* __restrict__ mean,
+                                const float* __restrict__ stdv, const float* __restrict__ gamma,
+                                const float* __restrict__ beta, const float* __restrict__ res, float* __restrict__ out) {
+    const size_t n = (size_t)R * C;
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
+        const int r = (int)(e / C), c = (int)(e % C);
+        const size_t o = (size_t)r * ld + c;
+        float v = ((Y[o] - mean[c]) / stdv[c]) * gamma[c] + beta[c];
+        if (res) v += res[o];
+        out[o] = fmaxf(v, 0.0f);
+    }
+}
+
+// BN backward: dy = (gamma/std) * (dz - dbeta/R - yhat*dgamma/R), dz = dout*(o > 0);
+// if dres: dres = dz (the residual branch's gradient, added by the next data-grad GEMM)
+__global__ void bn_back_kernel(const float* __restrict__ dout, const float* __restrict__ O, const float* __restrict__ Y,
+                               int ld, int C, int R, const float* __restrict__ mean, const float* __restrict__ stdv,
+                               const float* __restrict__ gamma, const float* __restrict__ dgamma,
+                               const float* __restrict__ dbeta, float* __restrict__ dy, float* __restrict__ dres) {
+    const size_t n = (size_t)R * C;
+    const float invR = 1.0f / (float)R;
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
+        const int r = (int)(e / C), c = (int)(e % C);
+        const size_t o = (size_t)r * ld + c;
+        const float dz = O[o] > 0.0f ? dout[o] : 0.0f;
+        const float yhat = (Y[o] - mean[c]) / stdv[c];
+        dy[o] = (gamma[c] / stdv[c]) * (dz - dbeta[c] * invR - yhat * dgamma[c] * invR);
+        if (dres) dres[o] = dz;
+    }
+}
+
+// planes [B][19][64] (to_tensor layout, chess.rs:191-245) -> X0 [B*64][64] (channels >= 19 zero)
+__global__ void planes_kernel(const float* __restrict__ planes, int B, float* __restrict__ x0) {
+    const size_t n = (size_t)B * 64 * 64;
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
+        const int c = (int)(e & 63), r = (int)(e >> 6), b = r >> 6, s = r & 63;
+        x0[e] = c < 19 ? planes[((size_t)b * 19 + c) * 64 + s] : 0.0f;
+    }
+}
+
+// value-head flatten (agent.rs:135: reshape [B, 8*8*8], index c*64 + s) and its inverse
+__global__ void vflat_kernel(float* __restrict__ a40, float* __restrict__ vflat, int B, int inverse) {
+    const size_t n = (size_t)B * 512;
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
+        const int b = (int)(e / 512), i = (int)(e % 512), c = i >> 6, s = i & 63;
+        const size_t o = ((size_t)b * 64 + s) * 64 + 32 + c;
+        if (inverse) a40[o] = vflat[e];
+        else vflat[e] = a40[o];
+    }
+}
+
+// ------------------------------------------------------------------ loss (training.rs:277-292)
+// One 256-thread block per board.  Policy: p = softmax(logits) over the 4096 flat entries
+// (index c*64 + s, agent.rs:126-129), loss_b = -sum t*log(p + 1e-5); dlogit = p*(G - sum p*G),
+// G = -t/(p + 1e-5)/B.  Value: v = tanh(relu(h1) . w2 + b2), loss_b = (v - z)^2,
+// dlogit_v = 0.5*2*(v - z)/B * (1 - v^2); dh1 = dlogit_v * w2 * (h1 > 0).
+// Per-board outputs: loss[b] = {policy, value}; vpart[b] = {dW2[64], db2}.
+__global__ void __launch_bounds__(256)
+loss_kernel(const float* __restrict__ logits, const float* __restrict__ tpol, const float* __restrict__ h1,
+            const float* __restrict__ tval, const float* __restrict__ w2, const float* __restrict__ b2, int B,
+            float* __restrict__ dlogits, float* __restrict__ dh1, float* __restrict__ loss,
+            float* __restrict__ vpart) {
+    __shared__ float red[256];
+    __shared__ float bc[4];
+    const int b = blockIdx.x, t = threadIdx.x;
+    const float* L = logits + (size_t)b * 64 * 64;
+    const float* T = tpol + (size_t)b * 4096;
+    float l[16];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const int i = t + 256 * j;
+        l[j] = L[(i & 63) * 64 + (i >> 6)];
+        mx = fmaxf(mx, l[j]);
+    }
+    auto block_reduce = [&](float v, bool is_max) -> float {
+        red[t] = v;
+        __syncthreads();
+        for (int o = 128; o > 0; o >>= 1) {
+            if (t < o) red[t] = is_max ? fmaxf(red[t], red[t + o]) : red[t] + red[t + o];
+            __syncthreads();
+        }
+        const float r = red[0];
+        __syncthreads();
+        return r;
+    };
+    mx = block_reduce(mx, true);
+    float se = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 16; j++) { l[j] = expf(l[j] - mx); se += l[j]; }
+    se = block_reduce(se, false);
+    const float invB = 1.0f / (float)B;
+    float lp = 0.0f, pg = 0.0f, G[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const int i = t + 256 * j;
+        const float p = l[j] / se, q = T[i];
+        l[j] = p;
+        lp += q * logf(p + 1e-5f);
+        G[j] = -q / (p + 1e-5f) * invB;
+        pg += p * G[j];
+    }
+    lp = block_reduce(lp, false);
+    pg = block_reduce(pg, false);
+    float* D = dlogits + (size_t)b * 64 * 64;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const int i = t + 256 * j;
+        D[(i & 63) * 64 + (i >> 6)] = l[j] * (G[j] - pg);
+    }
+    // value tail
+    const float hv = t < 64 ? h1[(size_t)b * 64 + t] : 0.0f;
+    const float a = fmaxf(hv, 0.0f);
+    const float dot = block_reduce(t < 64 ? a * w2[t] : 0.0f, false);
+    if (t == 0) {
+        const float v = tanhf(dot + b2[0]);
+        const float d = v - tval[b];
+        bc[0] = d * 2.0f * 0.5f * invB * (1.0f - v * v);
+        loss[b * 2 + 0] = -lp;
+        loss[b * 2 + 1] = d * d;
+    }
+    __syncthreads();
+    const float dl = bc[0];
+    if (t < 64) {
+        dh1[(size_t)b * 64 + t] = hv > 0.0f ? dl * w2[t] : 0.0f;
+        vpart[(size_t)b * 65 + t] = dl * a;
+    }
+    if (t == 0) vpart[(size_t)b * 65 + 64] = dl;
+}
+
+// ------------------------------------------------------------------ weight repacking
+// conv [co][ci][3][3] (burn) -> Wf[t][k][co] (k < kpad, rows >= cin zero) and Wd[t][co][ci] = Wf[8-t]^T
+__global__ void repack3x3_kernel(const float* __restrict__ w, int co_n, int ci_n, int kpad, float* __restrict__ wf,
+                                 float* __restrict__ wd) {
+    const size_t n = (size_t)9 * kpad * co_n;
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
+        const int co = (int)(e % co_n), k = (int)((e / co_n) % kpad), t = (int)(e / ((size_t)co_n * kpad));
+        const float v = k < ci_n ? w[((size_t)co * ci_n + k) * 9 + t] : 0.0f;
+        wf[e] = v;
+        if (wd && k < ci_n) wd[((size_t)(8 - t) * co_n + co) * ci_n + k] = v;
+    }
+}
+
+// dWf[t][k][co] -> grad [co][ci][3][3]
+__global__ void unpack3x3_kernel(const float* __restrict__ dwf, int co_n, int ci_n, int kpad, float* __restrict__ g) {
+    const size_t n = (size_t)co_n * ci_n * 9;
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
+        const int t = (int)(e % 9), ci = (int)((e / 9) % ci_n), co = (int)(e / ((size_t)9 * ci_n));
+        g[e] = dwf[((size_t)t * kpad + ci) * co_n + co];
+    }
+}
+
+// generic 2-D transpose with zero padding: dst[c][r] (ld_dst) = src[r][c] for r < rows, c < cols
+__global__ void transpose_kernel(const float* __restrict__ src, int rows, int cols, float* __restrict__ dst, int ld_dst,
+                                 int dst_rows) {
+    const size_t n = (size_t)dst_rows * ld_dst;
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
+        const int c = (int)(e / ld_dst), r = (int)(e % ld_dst);
+        dst[e] = (c < cols && r < rows) ? src[(size_t)r * cols + c] : 0.0f;
+    }
+}
+
+// ------------------------------------------------------------------ optimizer
+// burn AdamW with GradientClipping::Value(1.0): g = clamp(grad*scale, -1, 1);
+// m = b1*m + (1-b1)*g; v = b2*v + (1-b2)*g^2; update = (m/bc1) / (sqrt(v/bc2) + eps);
+// p = p*(1 - lr*wd) - lr*update.  Running statistics (mask 0) are not parameters.
+__global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                             float* __restrict__ v, const uint8_t* __restrict__ mask, size_t n, float gscale,
+                             float decay_mul, float lr, float bc1, float bc2) {
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
+        if (!mask[e]) continue;
+        const float gr = fminf(fmaxf(g[e] * gscale, -1.0f), 1.0f);
+        const float m1 = m[e] * 0.9f + gr * (1.0f - 0.9f);
+        const float m2 = v[e] * 0.999f + (gr * gr) * (1.0f - 0.999f);
+        m[e] = m1;
+        v[e] = m2;
+        const float upd = (m1 / bc1) / (sqrtf(m2 / bc2) + 1e-5f);
+        p[e] = p[e] * decay_mul - upd * lr;
+    }
+}
+
+// gather / scatter the running statistics (mask 2) into a contiguous buffer for the all-reduce
+__global__ void stats_pack_kernel(float* __restrict__ p, const uint32_t* __restrict__ idx, int n, float* __restrict__ buf,
+                                  int unpack, float scale) {
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+        if (unpack) p[idx[e]] = buf[e] * scale;
+        else buf[e] = p[idx[e]];
+    }
+}
+
+}  // namespace tr
+
+// ====================================================================== host side
+namespace {
+
+inline int grid_for(size_t n, int per = 256) {
+    size_t g = (n + per - 1) / per;
+    return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
+}
+
+struct Seg { size_t off, n; };
+
+// flat parameter layout of include/az.h (az_net_num_params; azchess.agent.param_shapes)
+struct Layout {
+    struct Conv { size_t w, b, bn; int cin, cout, k; };
+    std::vector<Conv> tower;          // input conv, then conv1/conv2 of every block
+    size_t p1w, p1b, pbn, p2w, p2b, vw, vb, vbn, l1w, l1b, l2w, l2b, total;
+    static Layout make(int B, int F) {
+        Layout L;
+        size_t o = 0;
+        auto conv = [&](int cin, int cout, int k) {
+            Conv c;
+            c.cin = cin; c.cout = cout; c.k = k;
+            c.w = o; o += (size_t)cout * cin * k * k;
+            c.b = o; o += cout;
+            c.bn = o; o += 4 * (size_t)cout;
+            return c;
+        };
+        L.tower.push_back(conv(19, F, 3));
+        for (int b = 0; b < 2 * B; b++) L.tower.push_back(conv(F, F, 3));
+        L.p1w = o; o += 32 * (size_t)F; L.p1b = o; o += 32; L.pbn = o; o += 4 * 32;
+        L.p2w = o; o += 64 * 32; L.p2b = o; o += 64;
+        L.vw = o; o += 8 * (size_t)F; L.vb = o; o += 8; L.vbn = o; o += 4 * 8;
+        L.l1w = o; o += 512 * 64; L.l1b = o; o += 64;
+        L.l2w = o; o += 64; L.l2b = o; o += 1;
+        L.total = o;
+        return L;
+    }
+};
+
+}  // namespace
+
+struct Trainer {
+    int blocks = 0, F = 0, Bmax = 0, device = 0;
+    hipStream_t st = nullptr;
+    Layout L;
+    size_t np = 0;
+    float *p = nullptr, *g = nullptr, *m = nullptr, *v = nullptr;
+    uint8_t* mask = nullptr;
+    long long t = 0;                         // AdamW time (burn AdaptiveMomentumWState::time)
+    int last_batch = 0;
+    // repacked weights
+    std::vector<float*> wf, wd;
+    float *w40f = nullptr, *w40d = nullptr, *b40 = nullptr, *wp2f = nullptr, *w1d = nullptr;
+    // saved activations (R = B*64 rows)
+    float* x0 = nullptr;                     // [R][64] input planes
+    std::vector<float*> xs, y1, hh, y2;      // xs[0..blocks], y1/hh/y2[blocks]
+    float *y0 = nullptr, *y40 = nullptr, *a40 = nullptr, *logits = nullptr, *vflat = nullptr, *h1 = nullptr;
+    // gradients of activations
+    float *dx = nullptr, *dxn = nullptr, *dres = nullptr, *dy = nullptr, *dh = nullptr;
+    float *da40 = nullptr, *dy40 = nullptr, *dlog = nullptr, *dvflat = nullptr, *dh1 = nullptr;
+    // per-BN statistics kept for backward: mean/std [nbn][F]
+    float *bmean = nullptr, *bstd = nullptr, *dgb = nullptr;
+    // reduction scratch
+    float *wpart = nullptr, *cpart = nullptr, *dwtmp = nullptr;
+    size_t wpart_cap = 0, dwtmp_cap = 0;
+    int slot = 0;                            // per-BN statistics stride (>= every BN's channels)
+    float *tpol = nullptr, *tval = nullptr, *planes = nullptr, *loss = nullptr, *vpart = nullptr;
+    float* hloss = nullptr;                  // pinned [Bmax][2]
+    // data parallel
+    ncclComm_t comm = nullptr;
+    int rank = 0, world = 1;
+    uint32_t* stat_idx = nullptr; float* stat_buf = nullptr; int nstat = 0;
+    std::vector<void*> allocs;
+
+    float* alloc(size_t n) {
+        void* q = nullptr;
+        if (hipMalloc(&q, n * sizeof(float) + 16) != hipSuccess) return nullptr;
+        allocs.push_back(q);
+        return reinterpret_cast<float*>(q);
+    }
+    ~Trainer() {
+        if (comm) ncclCommDestroy(comm);
+        for (void* q : allocs) (void)hipFree(q);
+        if (hloss) (void)hipHostFree(hloss);
+        if (st) (void)hipStreamDestroy(st);
+    }
+};
+
+namespace {
+
+constexpr int ROWS_PER_SPLIT = 512;   // weight-grad row split (8 boards)
+
+int launch_conv(Trainer* T, int taps, const float* X, int ldx, int K, const float* W, int N, const float* bias,
+                const float* addend, float* Y, int ldy, int R) {
+    if (K % 16 || N % 16 || ldx % 4 || ldy % 4 || (taps == 9 && R % 64)) return fail("conv: bad shape");
+    dim3 grid((R + tr::CM - 1) / tr::CM, (N + tr::CN - 1) / tr::CN);
+    if (taps == 9) tr::conv_f32_kernel<9><<<grid, 256, 0, T->st>>>(X, ldx, K, W, N, bias, addend, Y, ldy, R);
+    else tr::conv_f32_kernel<1><<<grid, 256, 0, T->st>>>(X, ldx, K, W, N, bias, addend, Y, ldy, R);
+    return hipGetLastError() == hipSuccess ? 0 : fail("conv launch failed");
+}
+
+// dW[taps][K][N] = sum_r X[r+d_t][k] * DY[r][n]
+int wgrad_rows_per_split(int taps, int R) { return taps == 9 || R >= 4096 ? ROWS_PER_SPLIT : 64; }
+size_t wgrad_splits(int taps, int R) {
+    const int rps = wgrad_rows_per_split(taps, R);
+    return (size_t)((R + rps - 1) / rps);
+}
+
+// out_cap: elements the destination holds (taps*K*N must fit)
+int launch_wgrad(Trainer* T, int taps, const float* X, int ldx, int K, const float* DY, int ldd, int N, int R,
+                 float* out, size_t out_cap) {
+    if (ldx % 4 || ldd % 4 || K % 4 || N % 16 || (taps == 9 && R % 64)) return fail("wgrad: bad shape");
+    if ((size_t)taps * K * N > out_cap) return fail("wgrad: destination too small");
+    if (wgrad_splits(taps, R) * taps * K * N > T->wpart_cap) return fail("wgrad: partial buffer too small");
+    const int rps = wgrad_rows_per_split(taps, R);
+    const int splits = (int)wgrad_splits(taps, R);
+    dim3 grid((K + tr::GK - 1) / tr::GK, (N + tr::GN - 1) / tr::GN, splits);
+    if (taps == 9) tr::wgrad_f32_kernel<9><<<grid, 256, 0, T->st>>>(X, ldx, K, DY, ldd, N, R, rps, T->wpart);
+    else tr::wgrad_f32_kernel<1><<<grid, 256, 0, T->st>>>(X, ldx, K, DY, ldd, N, R, rps, T->wpart);
+    const size_t n = (size_t)taps * K * N;
+    tr::reduce_kernel<<<grid_for(n), 256, 0, T->st>>>(T->wpart, splits, n, out);
+    return hipGetLastError() == hipSuccess ? 0 : fail("wgrad launch failed");
+}
+
+int nblk_rows(int R) { return (R + tr::CS_ROWS - 1) / tr::CS_ROWS; }
+
+// BatchNorm (training) + ReLU (+ residual): Y -> out; saves mean/std in slot `bi`
+int bn_forward(Trainer* T, int bi, const float* Y, int ld, int C, int R, size_t bn_off, const float* res, float* out) {
+    float* P = T->p + bn_off;   // {gamma, beta, running_mean, running_var}
+    if (C > T->slot) return fail("bn: too many channels");
+    float* mean = T->bmean + (size_t)bi * T->slot;
+    float* sd = T->bstd + (size_t)bi * T->slot;
+    const int nb = nblk_rows(R);
+    dim3 g(nb, (C + 63) / 64);
+    tr::colsum_kernel<0><<<g, 256, 0, T->st>>>(Y, ld, C, R, nullptr, nullptr, nullptr, nullptr, T->cpart);
+    tr::finalize_mean_kernel<<<(C + 255) / 256, 256, 0, T->st>>>(T->cpart, nb, C, R, mean);
+    tr::colsum_kernel<1><<<g, 256, 0, T->st>>>(Y, ld, C, R, mean, nullptr, nullptr, nullptr, T->cpart);
+    tr::finalize_var_kernel<<<(C + 255) / 256, 256, 0, T->st>>>(T->cpart, nb, C, R, mean, sd, P + 2 * C, P + 3 * C);
+    tr::bn_apply_kernel<<<grid_for((size_t)R * C), 256, 0, T->st>>>(Y, ld, C, R, mean, sd, P, P + C, res, out);
+    return hipGetLastError() == hipSuccess ? 0 : fail("bn forward failed");
+}
+
+// BN backward: dout (grad of the ReLU output O), pre-BN Y -> dy; dgamma/dbeta into the grad buffer
+int bn_backward(Trainer* T, int bi, const float* dout, const float* O, const float* Y, int ld, int C, int R,
+                size_t bn_off, float* dy, float* dres) {
+    const float* mean = T->bmean + (size_t)bi * T->slot;
+    const float* sd = T->bstd + (size_t)bi * T->slot;
+    const int nb = nblk_rows(R);
+    dim3 g(nb, (C + 63) / 64);
+    tr::colsum_kernel<2><<<g, 256, 0, T->st>>>(dout, ld, C, R, mean, sd, O, Y, T->cpart);
+    float* dgam = T->g + bn_off;
+    float* dbet = T->g + bn_off + C;
+    tr::finalize_bnback_kernel<<<(C + 255) / 256, 256, 0, T->st>>>(T->cpart, nb, C, dgam, dbet);
+    tr::bn_back_kernel<<<grid_for((size_t)R * C), 256, 0, T->st>>>(dout, O, Y, ld, C, R, mean, sd, T->p + bn_off, dgam,
+                                                                   dbet, dy, dres);
+    return hipGetLastError() == hipSuccess ? 0 : fail("bn backward failed");
+}
+
+int bias_grad(Trainer* T, const float* dy, int ld, int C, int R, float* dst) {
+    const int nb = nblk_rows(R);
+    dim3 g(nb, (C + 63) / 64);
+    tr::colsum_kernel<0><<<g, 256, 0, T->st>>>(dy, ld, C, R, nullptr, nullptr, nullptr, nullptr, T->cpart);
+    tr::finalize_sum_kernel<<<(C + 255) / 256, 256, 0, T->st>>>(T->cpart, nb, C, dst);
+    return hipGetLastError() == hipSuccess ? 0 : fail("bias grad failed");
+}
+
+#define TRY(x) do { if ((x) != 0) return -1; } while (0)
+
+int trainer_grads(Trainer* T, const float* planes, const float* tpol, const float* tval, int B, float* losses) {
+    if (B < 1 || B > T->Bmax) return fail("train: batch size out of range");
+    T->last_batch = B;
+    AZ_HIP(hipSetDevice(T->device));
+    const int F = T->F, R = B * 64;
+    hipStream_t st = T->st;
+    const Layout& L = T->L;
+    AZ_HIP(hipMemcpyAsync(T->planes, planes, (size_t)B * 19 * 64 * sizeof(float), hipMemcpyHostToDevice, st));
+    AZ_HIP(hipMemcpyAsync(T->tpol, tpol, (size_t)B * 4096 * sizeof(float), hipMemcpyHostToDevice, st));
+    AZ_HIP(hipMemcpyAsync(T->tval, tval, (size_t)B * sizeof(float), hipMemcpyHostToDevice, st));
+    AZ_HIP(hipMemsetAsync(T->g, 0, T->np * sizeof(float), st));
+    // weights of this step in GEMM layouts
+    for (size_t i = 0; i < L.tower.size(); i++) {
+        const auto& c = L.tower[i];
+        const int kpad = i == 0 ? 64 : F;
+        tr::repack3x3_kernel<<<grid_for((size_t)9 * kpad * F), 256, 0, st>>>(T->p + c.w, F, c.cin, kpad, T->wf[i],
+                                                                           i == 0 ? nullptr : T->wd[i]);
+    }
+    // heads 1x1 (policy_conv_1 | value_conv): w40d [64][F] = the two burn weights stacked
+    // (rows >= 40 zero), w40f [F][64] its transpose
+    AZ_HIP(hipMemsetAsync(T->w40d, 0, (size_t)64 * F * sizeof(float), st));
+    AZ_HIP(hipMemcpyAsync(T->w40d, T->p + L.p1w, (size_t)32 * F * sizeof(float), hipMemcpyDeviceToDevice, st));
+    AZ_HIP(hipMemcpyAsync(T->w40d + (size_t)32 * F, T->p + L.vw, (size_t)8 * F * sizeof(float), hipMemcpyDeviceToDevice, st));
+    tr::transpose_kernel<<<grid_for((size_t)F * 64), 256, 0, st>>>(T->w40d, 64, F, T->w40f, 64, F);
+    AZ_HIP(hipMemsetAsync(T->b40, 0, 64 * sizeof(float), st));
+    AZ_HIP(hipMemcpyAsync(T->b40, T->p + L.p1b, 32 * sizeof(float), hipMemcpyDeviceToDevice, st));
+    AZ_HIP(hipMemcpyAsync(T->b40 + 32, T->p + L.vb, 8 * sizeof(float), hipMemcpyDeviceToDevice, st));
+    // policy_conv_2 [64][32] -> wp2f [32][64]; its data grad uses the burn layout as is
+    tr::transpose_kernel<<<grid_for(32 * 64), 256, 0, st>>>(T->p + L.p2w, 64, 32, T->wp2f, 64, 32);
+    // value_linear_1 [512][64] is already [K][N]; data grad needs [64][512]
+    tr::transpose_kernel<<<grid_for(512 * 64), 256, 0, st>>>(T->p + L.l1w, 512, 64, T->w1d, 512, 64);
+
+    // ---------------- forward (agent.rs:112-144, training-mode BatchNorm)
+    tr::planes_kernel<<<grid_for((size_t)R * 64), 256, 0, st>>>(T->planes, B, T->x0);
+    TRY(launch_conv(T, 9, T->x0, 64, 64, T->wf[0], F, T->p + L.tower[0].b, nullptr, T->y0, F, R));
+    TRY(bn_forward(T, 0, T->y0, F, F, R, L.tower[0].bn, nullptr, T->xs[0]));
+    for (int b = 0; b < T->blocks; b++) {
+        const auto& c1 = L.tower[1 + 2 * b];
+        const auto& c2 = L.tower[2 + 2 * b];
+        TRY(launch_conv(T, 9, T->xs[b], F, F, T->wf[1 + 2 * b], F, T->p + c1.b, nullptr, T->y1[b], F, R));
+        TRY(bn_forward(T, 1 + 2 * b, T->y1[b], F, F, R, c1.bn, nullptr, T->hh[b]));
+        TRY(launch_conv(T, 9, T->hh[b], F, F, T->wf[2 + 2 * b], F, T->p + c2.b, nullptr, T->y2[b], F, R));
+        TRY(bn_forward(T, 2 + 2 * b, T->y2[b], F, F, R, c2.bn, T->xs[b], T->xs[b + 1]));
+    }
+    const float* body = T->xs[T->blocks];
+    const int nbn = 1 + 2 * T->blocks;
+    TRY(launch_conv(T, 1, body, F, F, T->w40f, 64, T->b40, nullptr, T->y40, 64, R));
+    AZ_HIP(hipMemsetAsync(T->a40, 0, (size_t)R * 64 * sizeof(float), st));
+    TRY(bn_forward(T, nbn, T->y40, 64, 32, R, L.pbn, nullptr, T->a40));
+    TRY(bn_forward(T, nbn + 1, T->y40 + 32, 64, 8, R, L.vbn, nullptr, T->a40 + 32));
+    TRY(launch_conv(T, 1, T->a40, 64, 32, T->wp2f, 64, T->p + L.p2b, nullptr, T->logits, 64, R));
+    tr::vflat_kernel<<<grid_for((size_t)B * 512), 256, 0, st>>>(T->a40, T->vflat, B, 0);
+    TRY(launch_conv(T, 1, T->vflat, 512, 512, T->p + L.l1w, 64, T->p + L.l1b, nullptr, T->h1, 64, B));
+    // ---------------- loss + head tails
+    tr::loss_kernel<<<B, 256, 0, st>>>(T->logits, T->tpol, T->h1, T->tval, T->p + L.l2w, T->p + L.l2b, B, T->dlog,
+                                       T->dh1, T->loss, T->vpart);
+    {   // value_linear_2 grads: sum over boards of the per-board partials
+        const int nb = nblk_rows(B);
+        dim3 g(nb, 2);
+        tr::colsum_kernel<0><<<g, 256, 0, st>>>(T->vpart, 65, 65, B, nullptr, nullptr, nullptr, nullptr, T->cpart);
+        tr::finalize_sum_kernel<<<1, 128, 0, st>>>(T->cpart, nb, 65, T->dwtmp);
+        AZ_HIP(hipMemcpyAsync(T->g + L.l2w, T->dwtmp, 64 * sizeof(float), hipMemcpyDeviceToDevice, st));
+        AZ_HIP(hipMemcpyAsync(T->g + L.l2b, T->dwtmp + 64, sizeof(float), hipMemcpyDeviceToDevice, st));
+    }
+    // ---------------- backward
+    // value_linear_1
+    TRY(launch_wgrad(T, 1, T->vflat, 512, 512, T->dh1, 64, 64, B, T->g + L.l1w, 512 * 64));
+    TRY(bias_grad(T, T->dh1, 64, 64, B, T->g + L.l1b));
+    TRY(launch_conv(T, 1, T->dh1, 64, 64, T->w1d, 512, nullptr, nullptr, T->dvflat, 512, B));
+    // policy_conv_2: dW[32][64] -> grad [64][32]
+    TRY(launch_wgrad(T, 1, T->a40, 64, 32, T->dlog, 64, 64, R, T->dwtmp, T->dwtmp_cap));
+    tr::transpose_kernel<<<grid_for(64 * 32), 256, 0, st>>>(T->dwtmp, 32, 64, T->g + L.p2w, 32, 64);
+    TRY(bias_grad(T, T->dlog, 64, 64, R, T->g + L.p2b));
+    AZ_HIP(hipMemsetAsync(T->da40, 0, (size_t)R * 64 * sizeof(float), st));
+    TRY(launch_conv(T, 1, T->dlog, 64, 64, T->p + L.p2w, 32, nullptr, nullptr, T->da40, 64, R));
+    tr::vflat_kernel<<<grid_for((size_t)B * 512), 256, 0, st>>>(T->da40, T->dvflat, B, 1);
+    // head BatchNorms -> dy40 (cols >= 40 stay zero)
+    AZ_HIP(hipMemsetAsync(T->dy40, 0, (size_t)R * 64 * sizeof(float), st));
+    TRY(bn_backward(T, nbn, T->da40, T->a40, T->y40, 64, 32, R, L.pbn, T->dy40, nullptr));
+    TRY(bn_backward(T, nbn + 1, T->da40 + 32, T->a40 + 32, T->y40 + 32, 64, 8, R, L.vbn, T->dy40 + 32, nullptr));
+    // heads 1x1: dW[F][64] -> policy_conv_1 [32][F], value_conv [8][F]
+    TRY(launch_wgrad(T, 1, body, F, F, T->dy40, 64, 64, R, T->dwtmp, (size_t)F * 64));
+    tr::transpose_kernel<<<grid_for((size_t)40 * F), 256, 0, st>>>(T->dwtmp, F, 64, T->dwtmp + (size_t)F * 64, F, 40);
+    AZ_HIP(hipMemcpyAsync(T->g + L.p1w, T->dwtmp + (size_t)F * 64, (size_t)32 * F * sizeof(float), hipMemcpyDeviceToDevice, st));
+    AZ_HIP(hipMemcpyAsync(T->g + L.vw, T->dwtmp + (size_t)F * 64 + (size_t)32 * F, (size_t)8 * F * sizeof(float),
+                          hipMemcpyDeviceToDevice, st));
+    TRY(bias_grad(T, T->dy40, 64, 32, R, T->g + L.p1b));
+    TRY(bias_grad(T, T->dy40 + 32, 64, 8, R, T->g + L.vb));
+    TRY(launch_conv(T, 1, T->dy40, 64, 64, T->w40d, F, nullptr, nullptr, T->dx, F, R));
+    // residual tower, last block first
+    for (int b = T->blocks - 1; b >= 0; b--) {
+        const auto& c1 = L.tower[1 + 2 * b];
+        const auto& c2 = L.tower[2 + 2 * b];
+        TRY(bn_backward(T, 2 + 2 * b, T->dx, T->xs[b + 1], T->y2[b], F, F, R, c2.bn, T->dy, T->dres));
+        TRY(bias_grad(T, T->dy, F, F, R, T->g + c2.b));
+        TRY(launch_wgrad(T, 9, T->hh[b], F, F, T->dy, F, F, R, T->dwtmp, T->dwtmp_cap));
+        tr::unpack3x3_kernel<<<grid_for((size_t)9 * F * F), 256, 0, st>>>(T->dwtmp, F, F, F, T->g + c2.w);
+        TRY(launch_conv(T, 9, T->dy, F, F, T->wd[2 + 2 * b], F, nullptr, nullptr, T->dh, F, R));
+        TRY(bn_backward(T, 1 + 2 * b, T->dh, T->hh[b], T->y1[b], F, F, R, c1.bn, T->dy, nullptr));
+        TRY(bias_grad(T, T->dy, F, F, R, T->g + c1.b));
+        TRY(launch_wgrad(T, 9, T->xs[b], F, F, T->dy, F, F, R, T->dwtmp, T->dwtmp_cap));
+        tr::unpack3x3_kernel<<<grid_for((size_t)9 * F * F), 256, 0, st>>>(T->dwtmp, F, F, F, T->g + c1.w);
+        TRY(launch_conv(T, 9, T->dy, F, F, T->wd[1 + 2 * b], F, nullptr, T->dres, T->dxn, F, R));
+        std::swap(T->dx, T->dxn);
+    }
+    // input conv (no data grad)
+    TRY(bn_backward(T, 0, T->dx, T->xs[0], T->y0, F, F, R, L.tower[0].bn, T->dy, nullptr));
+    TRY(bias_grad(T, T->dy, F, F, R, T->g + L.tower[0].b));
+    TRY(launch_wgrad(T, 9, T->x0, 64, 64, T->dy, F, F, R, T->dwtmp, T->dwtmp_cap));
+    tr::unpack3x3_kernel<<<grid_for((size_t)9 * 19 * F), 256, 0, st>>>(T->dwtmp, F, 19, 64, T->g + L.tower[0].w);
+    AZ_HIP(hipMemcpyAsync(T->hloss, T->loss, (size_t)B * 2 * sizeof(float), hipMemcpyDeviceToHost, st));
+    AZ_HIP(hipStreamSynchronize(st));
+    if (losses) {   // training.rs:281-282: means over the batch (policy, value)
+        double pl = 0.0, vl = 0.0;
+        for (int i = 0; i < B; i++) { pl += T->hloss[2 * i]; vl += T->hloss[2 * i + 1]; }
+        losses[0] = (float)(pl / B);
+        losses[1] = (float)(vl / B);
+    }
+    return 0;
+}
+
+float powi_f32(float x, long long n) {   // Rust f32::powi (repeated squaring in f32)
+    float r = 1.0f;
+    while (n > 0) { if (n & 1) r *= x; x *= x; n >>= 1; }
+    return r;
+}
+
+int trainer_apply(Trainer* T, double lr) {
+    AZ_HIP(hipSetDevice(T->device));
+    hipStream_t st = T->st;
+    if (T->comm && T->world > 1) {
+        if (ncclAllReduce(T->g, T->g, T->np, ncclFloat, ncclSum, T->comm, st) != ncclSuccess)
+            return fail("ncclAllReduce (gradients) failed");
+    }
+    T->t++;
+    const float bc1 = 1.0f - powi_f32(0.9f, T->t), bc2 = 1.0f - powi_f32(0.999f, T->t);
+    const float decay_mul = (float)(1.0 - lr * 1e-4);   // WEIGHT_DECAY, parameters.rs:25
+    tr::adamw_kernel<<<grid_for(T->np), 256, 0, st>>>(T->p, T->g, T->m, T->v, T->mask, T->np, 1.0f / (float)T->world,
+                                                       decay_mul, (float)lr, bc1, bc2);
+    if (T->comm && T->world > 1) {   // average the BatchNorm running statistics over ranks
+        tr::stats_pack_kernel<<<grid_for(T->nstat), 256, 0, st>>>(T->p, T->stat_idx, T->nstat, T->stat_buf, 0, 1.0f);
+        if (ncclAllReduce(T->stat_buf, T->stat_buf, T->nstat, ncclFloat, ncclSum, T->comm, st) != ncclSuccess)
+            return fail("ncclAllReduce (running statistics) failed");
+        tr::stats_pack_kernel<<<grid_for(T->nstat), 256, 0, st>>>(T->p, T->stat_idx, T->nstat, T->stat_buf, 1,
+                                                                  1.0f / (float)T->world);
+    }
+    AZ_HIP(hipGetLastError());
+    AZ_HIP(hipStreamSynchronize(st));
+    return 0;
+}
+
+}  // namespace
+}  // namespace azi
+
+struct az_trainer { azi::Trainer* t; };
+
+using namespace azi;
+
+extern "C" {
+
+double az_cyclical_lr(int iteration) {   // get_cyclical_lr, training.rs:424-441 (parameters.rs:20-24)
+    const int decay_factor = iteration / 1000;
+    const double mult = pow(10.0, -(double)decay_factor);
+    const double base = 1e-3 * mult, mx = 1e-2 * mult;
+    const int cur = iteration % 20;
+    const double range = mx - base;
+    if (cur <= 10) return base + (double)cur / 10.0 * range;
+    return mx - (double)(cur - 10) / 10.0 * range;
+}
+
+int az_trainer_create(int blocks, int filters, const float* weights, size_t n, int max_batch, int device,
+                      az_trainer** out) {
+    if (!out || !weights || blocks < 0 || blocks > 40 || filters < 16 || filters % 16 || max_batch < 1)
+        return fail("az_trainer_create: bad arguments (filters must be a multiple of 16)");
+    if (n != az_net_num_params(blocks, filters)) return fail("az_trainer_create: weight count mismatch");
+    AZ_HIP(hipSetDevice(device));
+    Trainer* T = new Trainer();
+    T->blocks = blocks; T->F = filters; T->Bmax = max_batch; T->device = device;
+    T->L = Layout::make(blocks, filters);
+    T->np = T->L.total;
+    const int F = filters;
+    const size_t R = (size_t)max_batch * 64;
+    bool ok = hipStreamCreateWithFlags(&T->st, hipStreamNonBlocking) == hipSuccess;
+    auto A = [&](size_t k) { float* q = T->alloc(k); ok = ok && q; return q; };
+    T->p = A(T->np); T->g = A(T->np); T->m = A(T->np); T->v = A(T->np);
+    void* mk = nullptr;
+    ok = ok && hipMalloc(&mk, T->np) == hipSuccess;
+    if (mk) T->allocs.push_back(mk);
+    T->mask = reinterpret_cast<uint8_t*>(mk);
+    const int nconv = 1 + 2 * blocks;
+    for (int i = 0; i < nconv; i++) {
+        T->wf.push_back(A((size_t)9 * (i == 0 ? 64 : F) * F));
+        T->wd.push_back(i == 0 ? nullptr : A((size_t)9 * F * F));
+    }
+    T->w40f = A((size_t)F * 64); T->w40d = A((size_t)64 * F); T->b40 = A(64); T->wp2f = A(32 * 64); T->w1d = A(64 * 512);
+    T->x0 = A(R * 64);
+    for (int b = 0; b <= blocks; b++) T->xs.push_back(A(R * F));
+    for (int b = 0; b < blocks; b++) { T->y1.push_back(A(R * F)); T->hh.push_back(A(R * F)); T->y2.push_back(A(R * F)); }
+    T->y0 = A(R * F); T->y40 = A(R * 64); T->a40 = A(R * 64); T->logits = A(R * 64);
+    T->vflat = A((size_t)max_batch * 512); T->h1 = A((size_t)max_batch * 64);
+    T->dx = A(R * F); T->dxn = A(R * F); T->dres = A(R * F); T->dy = A(R * F); T->dh = A(R * F);
+    T->da40 = A(R * 64); T->dy40 = A(R * 64); T->dlog = A(R * 64);
+    T->dvflat = A((size_t)max_batch * 512); T->dh1 = A((size_t)max_batch * 64);
+    T->slot = std::max(F, 64);
+    T->bmean = A((size_t)(nconv + 2) * T->slot); T->bstd = A((size_t)(nconv + 2) * T->slot);
+    // weight-grad partials: the largest split count x output size over every wgrad launch
+    // (split counts grow with the row count, so the maximum is at max_batch)
+    const size_t s9 = wgrad_splits(9, (int)R), s1 = wgrad_splits(1, (int)R), sl = wgrad_splits(1, max_batch);
+    size_t wp = s9 * 9 * 64 * (size_t)F;                                // input conv
+    wp = std::max(wp, s9 * 9 * (size_t)F * F);                          // residual convs
+    wp = std::max(wp, s1 * (size_t)F * 64);                             // heads 1x1
+    wp = std::max(wp, s1 * 32 * 64);                                    // policy_conv_2
+    wp = std::max(wp, sl * 512 * 64);                                   // value_linear_1
+    T->wpart = A(wp);
+    T->wpart_cap = wp;
+    T->cpart = A((R / tr::CS_ROWS + 2) * 2 * (size_t)std::max(F, 65));
+    // dW scratch: input conv [9][64][F], residual conv [9][F][F], heads [F][64] + its [40][F]
+    // transpose, policy_conv_2 [32][64], value_linear_2 partial sums (65)
+    T->dwtmp_cap = std::max({(size_t)9 * 64 * F, (size_t)9 * F * F, (size_t)F * 64 + 40 * (size_t)F, (size_t)32 * 64,
+                             (size_t)65});
+    T->dwtmp = A(T->dwtmp_cap);
+    T->planes = A((size_t)max_batch * 19 * 64); T->tpol = A((size_t)max_batch * 4096); T->tval = A(max_batch);
+    T->loss = A((size_t)max_batch * 2); T->vpart = A((size_t)max_batch * 65);
+    ok = ok && hipHostMalloc((void**)&T->hloss, (size_t)max_batch * 2 * sizeof(float), 0) == hipSuccess;
+    if (!ok) { delete T; return fail("az_trainer_create: out of device memory"); }
+    // parameters, zero moments, trainable mask (BatchNorm running statistics are not parameters)
+    std::vector<uint8_t> mask(T->np, 1);
+    std::vector<uint32_t> sidx;
+    auto bn_stats = [&](size_t off, int C) {
+        for (int c = 0; c < 2 * C; c++) { mask[off + 2 * C + c] = 0; sidx.push_back((uint32_t)(off + 2 * C + c)); }
+    };
+    for (const auto& c : T->L.tower) bn_stats(c.bn, c.cout);
+    bn_stats(T->L.pbn, 32);
+    bn_stats(T->L.vbn, 8);
+    T->nstat = (int)sidx.size();
+    T->stat_idx = reinterpret_cast<uint32_t*>(T->alloc(sidx.size()));
+    T->stat_buf = T->alloc(sidx.size());
+    if (!T->stat_idx || !T->stat_buf) { delete T; return fail("az_trainer_create: out of device memory"); }
+    if (hipMemcpy(T->p, weights, T->np * sizeof(float), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(T->mask, mask.data(), T->np, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(T->stat_idx, sidx.data(), sidx.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemset(T->m, 0, T->np * sizeof(float)) != hipSuccess || hipMemset(T->v, 0, T->np * sizeof(float)) != hipSuccess ||
+        hipMemset(T->g, 0, T->np * sizeof(float)) != hipSuccess) {
+        delete T;
+        return fail("az_trainer_create: upload failed");
+    }
+    *out = new az_trainer{T};
+    return 0;
+}
+
+int az_trainer_destroy(az_trainer* t) {
+    if (!t) return 0;
+    (void)hipSetDevice(t->t->device);
+    delete t->t;
+    delete t;
+    return 0;
+}
+
+int az_trainer_compute_grads(az_trainer* t, const float* planes, const float* target_policy,
+                             const float* target_value, int batch, float* losses) {
+    if (!t || !planes || !target_policy || !target_value) return fail("null");
+    return trainer_grads(t->t, planes, target_policy, target_value, batch, losses);
+}
+
+int az_trainer_apply(az_trainer* t, double lr) {
+    if (!t) return fail("null");
+    return trainer_apply(t->t, lr);
+}
+
+int az_trainer_step(az_trainer* t, const float* planes, const float* target_policy, const float* target_value,
+                    int batch, double lr, float* losses) {
+    if (!t || !planes || !target_policy || !target_value) return fail("null");
+    if (trainer_grads(t->t, planes, target_policy, target_value, batch, losses) != 0) return -1;
+    return trainer_apply(t->t, lr);
+}
+
+int az_trainer_get_params(az_trainer* t, float* out, size_t n) {
+    if (!t || !out || n != t->t->np) return fail("az_trainer_get_params: bad arguments");
+    AZ_HIP(hipSetDevice(t->t->device));
+    AZ_HIP(hipStreamSynchronize(t->t->st));
+    AZ_HIP(hipMemcpy(out, t->t->p, n * sizeof(float), hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int az_trainer_get_grads(az_trainer* t, float* out, size_t n) {
+    if (!t || !out || n != t->t->np) return fail("az_trainer_get_grads: bad arguments");
+    AZ_HIP(hipSetDevice(t->t->device));
+    AZ_HIP(hipStreamSynchronize(t->t->st));
+    AZ_HIP(hipMemcpy(out, t->t->g, n * sizeof(float), hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int az_trainer_relu_output(az_trainer* t, int layer, float* out, size_t n) {
+    if (!t || !out) return fail("null");
+    Trainer* T = t->t;
+    const size_t R = (size_t)T->last_batch * 64;
+    const float* src = nullptr;
+    size_t cnt = 0;
+    const int nt = 1 + 2 * T->blocks;
+    if (layer >= 0 && layer < nt) {           // x0, h0, x1, h1, ..., x_B (NHWC [R][F])
+        src = layer == 0 ? T->xs[0] : (layer % 2 ? T->hh[(layer - 1) / 2] : T->xs[layer / 2]);
+        cnt = R * T->F;
+    } else if (layer == nt) {                  // heads: [R][64], columns 0..39 live
+        src = T->a40; cnt = R * 64;
+    } else if (layer == nt + 1) {              // value_linear_1 output before its ReLU [B][64]
+        src = T->h1; cnt = (size_t)T->last_batch * 64;
+    } else {
+        return fail("az_trainer_relu_output: bad layer");
+    }
+    if (n != cnt) return fail("az_trainer_relu_output: size mismatch");
+    AZ_HIP(hipSetDevice(T->device));
+    AZ_HIP(hipStreamSynchronize(T->st));
+    AZ_HIP(hipMemcpy(out, src, cnt * sizeof(float), hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int az_comm_unique_id(void* out, int cap) {
+    if (!out || cap < (int)sizeof(ncclUniqueId)) return fail("az_comm_unique_id: need 128 bytes");
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return fail("ncclGetUniqueId failed");
+    memcpy(out, &id, sizeof(id));
+    return (int)sizeof(id);
+}
+
+int az_trainer_set_comm(az_trainer* t, const void* unique_id, int rank, int world) {
+    if (!t || !unique_id || world < 1 || rank < 0 || rank >= world) return fail("az_trainer_set_comm: bad arguments");
+    Trainer* T = t->t;
+    AZ_HIP(hipSetDevice(T->device));
+    if (T->comm) { ncclCommDestroy(T->comm); T->comm = nullptr; }
+    ncclUniqueId id;
+    memcpy(&id, unique_id, sizeof(id));
+    if (ncclCommInitRank(&T->comm, world, id, rank) != ncclSuccess) return fail("ncclCommInitRank failed");
+    T->rank = rank;
+    T->world = world;
+    return 0;
+}
+
+}  // extern "C"

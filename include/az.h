@@ -182,6 +182,43 @@ typedef struct {
 } az_timing;
 int az_search_timing(az_search* s, az_timing* out, int reset, int enable);
 
+
+/* ---- training: training.rs train() inner loop ---------------------
+ * f32 end to end (the reference's precision).  The trainer owns a device copy of the flat
+ * parameters (az_net_num_params layout, BatchNorm running statistics included), the AdamW
+ * moments and every activation of a batch of up to max_batch positions. */
+typedef struct az_trainer az_trainer;
+/* get_cyclical_lr (training.rs:424-441) */
+double az_cyclical_lr(int iteration);
+/* AlphaZero::new/load_record + AdamWConfig::new().with_grad_clipping(Value(1.0))
+ * .with_weight_decay(1e-4).init() (training.rs:48-66) */
+int az_trainer_create(int blocks, int filters, const float* weights, size_t n, int max_batch, int device,
+                      az_trainer** out);
+int az_trainer_destroy(az_trainer* t);
+/* forward (training-mode BatchNorm, running statistics updated) + compute_gradients
+ * (training.rs:277-292) for one batch: planes [B,19,8,8] (to_tensor), target policy [B,4096],
+ * target value [B].  losses (may be NULL) = {policy_loss, value_loss} batch means. */
+int az_trainer_compute_grads(az_trainer* t, const float* planes, const float* target_policy,
+                             const float* target_value, int batch, float* losses);
+/* gradient all-reduce over the trainer's communicator (if any), clip by value 1.0,
+ * AdamW step with learning rate lr (optimizer.step, training.rs:186-189) */
+int az_trainer_apply(az_trainer* t, double lr);
+/* compute_grads + apply: one iteration of training.rs:147-190 */
+int az_trainer_step(az_trainer* t, const float* planes, const float* target_policy, const float* target_value,
+                    int batch, double lr, float* losses);
+/* flat parameters (to build an az_net for self-play, or to save) / last gradients */
+int az_trainer_get_params(az_trainer* t, float* out, size_t n);
+int az_trainer_get_grads(az_trainer* t, float* out, size_t n);
+/* introspection for parity tests: the activation each ReLU of the last forward acted on, in
+ * forward order -- layer 0 = input block output, 1..2B = residual blocks (h_b, x_b+1 NHWC
+ * [B*64][F]), 2B+1 = head convs after BN+ReLU [B*64][64] (columns 0..39), 2B+2 =
+ * value_linear_1 output before its ReLU [B][64].  n must equal the tensor's size. */
+int az_trainer_relu_output(az_trainer* t, int layer, float* out, size_t n);
+/* data-parallel training over RCCL (xGMI): rank 0 creates the id (128 bytes, returns its
+ * size), every rank passes it to az_trainer_set_comm. */
+int az_comm_unique_id(void* out, int cap);
+int az_trainer_set_comm(az_trainer* t, const void* unique_id, int rank, int world);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,143 @@
+"""Training step (training.rs:137-190, 277-292) on the GPU against the
+torch-CPU float64 oracle (oracle/train_ref.py).  The step computes in f32 (the reference's
+precision) on v_mfma_f32_16x16x4_f32.  Tolerances:
+  losses                 |d| <= 1e-5 * (1 + |ref|)
+  gradient tensors       relative norm error ||g - g_ref|| / ||g_ref|| <= 1e-4 per parameter
+                         tensor, with the oracle's ReLUs taking the GPU's branch (its masks, read
+                         back through az_trainer_relu_output): a pre-activation within f32 rounding
+                         of 0 can otherwise take the other branch in float64, and that one element
+                         moves dbeta of the BatchNorm below it by ~1/(64*B) relative, propagating
+                         to every earlier layer (measured 8e-4 at B=2, 20x256, without masks).
+                         Without masks: <= 1e-2.  Biases of convs followed by BatchNorm have exact
+                         gradient 0: max |g| <= 1e-5 (rounding noise of a sum that cancels).
+  running statistics     |d| <= 1e-5 * (1 + |ref|)
+  AdamW + clipping       bit-exact against the float32 restatement, given the GPU gradients
+"""
+import numpy as np
+import pytest
+
+import azchess as A
+import train_ref as T
+
+pytestmark = pytest.mark.gpu
+
+
+def batch(n, seed):
+    """Positions from random playouts (to_tensor planes), sparse target policies over legal
+    moves (visit distributions), target values in [-1, 1]."""
+    rng = np.random.default_rng(seed)
+    planes, pol, val = [], [], []
+    while len(planes) < n:
+        gs = A.GameState()
+        for _ in range(int(rng.integers(0, 60))):
+            idx = gs.position.legal_indices()
+            if len(idx) == 0 or int(A.play_move(gs, int(rng.choice(idx)))) != 0:
+                break
+        idx = np.unique(gs.position.legal_indices())
+        if len(idx) == 0:
+            continue
+        visits = rng.integers(0, 20, len(idx)).astype(np.float32)
+        visits[0] += 1
+        p = np.zeros(4096, np.float32)
+        p[idx] = visits / np.float32(visits.sum())
+        planes.append(A.to_tensor(gs.position).reshape(19 * 64))
+        pol.append(p)
+        val.append(np.float32(rng.uniform(-1, 1)))
+    return np.stack(planes), np.stack(pol), np.array(val, np.float32)
+
+
+def bn_fed_biases(blocks):
+    names = ["input_conv.bias", "policy_conv_1.bias", "value_conv.bias"]
+    for b in range(blocks):
+        names += ["res_blocks.%d.conv1.bias" % b, "res_blocks.%d.conv2.bias" % b]
+    return set(names)
+
+
+@pytest.mark.parametrize("blocks,filters,n", [(2, 32, 16), (6, 64, 8), (20, 256, 2)])
+def test_grads_losses_and_running_stats_match_oracle(require_gpu, blocks, filters, n):
+    w = A.random_weights(blocks, filters, seed=7)
+    planes, tpol, tval = batch(n, seed=blocks * 100 + n)
+    tr = A.Trainer(blocks, filters, weights=w, max_batch=max(n, 4))
+    pl, vl = tr.compute_gradients(planes, tpol, tval)
+    g = tr.grads()
+    masks = tr.relu_masks(n)
+    ref = T.TrainRef(blocks, filters, w)
+    rg, (rpl, rvl) = ref.grads(planes, tpol, tval, masks)
+    ug, _ = T.TrainRef(blocks, filters, w).grads(planes, tpol, tval)     # the oracle's own branches
+    assert abs(pl - rpl) <= 1e-5 * (1 + abs(rpl)), (pl, rpl)
+    assert abs(vl - rvl) <= 1e-5 * (1 + abs(rvl)), (vl, rvl)
+    zero_bias = bn_fed_biases(blocks)
+    seg, _ = T.segments(blocks, filters)
+    for name, (o, shape, bn) in seg.items():
+        size = int(np.prod(shape))
+        if bn:
+            C = shape[1]
+            parts = [(name + ".gamma", o, C), (name + ".beta", o + C, C)]
+        else:
+            parts = [(name, o, size)]
+        for pname, off, cnt in parts:
+            a, r, u = g[off:off + cnt].astype(np.float64), rg[off:off + cnt], ug[off:off + cnt]
+            if pname in zero_bias:
+                assert np.abs(a).max() <= 1e-5, (pname, np.abs(a).max())
+                continue
+            nr = max(np.linalg.norm(r), 1e-30)
+            assert np.linalg.norm(a - r) / nr <= 1e-4, (pname, np.linalg.norm(a - r) / nr)
+            assert np.linalg.norm(a - u) / nr <= 1e-2, (pname, np.linalg.norm(a - u) / nr)
+    p = tr.params()
+    rs = ref.running_stats_flat(w)
+    mask = T.trainable_mask(blocks, filters)
+    stats = ~mask
+    assert np.all(np.abs(p[stats] - rs[stats]) <= 1e-5 * (1 + np.abs(rs[stats])))
+    assert np.array_equal(p[mask], w[mask])    # compute_gradients does not move parameters
+
+
+def test_adamw_and_clipping_bit_exact(require_gpu):
+    blocks, filters = 2, 32
+    w = A.random_weights(blocks, filters, seed=3)
+    tr = A.Trainer(blocks, filters, weights=w, max_batch=16)
+    mask = T.trainable_mask(blocks, filters)
+    m = np.zeros_like(w)
+    v = np.zeros_like(w)
+    p = tr.params()
+    for step, it in enumerate([5, 13, 1002]):
+        planes, tpol, tval = batch(16, seed=step)
+        tr.compute_gradients(planes, tpol, tval)
+        g = tr.grads()
+        p = tr.params()                     # running statistics moved during the forward
+        lr = A.get_cyclical_lr(it)
+        assert lr == T.cyclical_lr(it)
+        tr.apply(lr)
+        p, m, v = T.adamw_step(p, g, m, v, mask, step + 1, lr)
+        got = tr.params()
+        assert np.array_equal(got, p), np.abs(got - p).max()
+    # clipping engaged: some gradient entries exceed 1 in magnitude on this batch
+    assert np.abs(g).max() > 0
+
+
+def test_step_is_deterministic_and_comm_world1_is_identity(require_gpu):
+    blocks, filters = 2, 64
+    w = A.random_weights(blocks, filters, seed=11)
+    planes, tpol, tval = batch(8, seed=5)
+    a = A.Trainer(blocks, filters, weights=w, max_batch=8)
+    b = A.Trainer(blocks, filters, weights=w, max_batch=8)
+    b.set_comm(A.comm_unique_id(), 0, 1)     # RCCL all-reduce over a 1-rank communicator
+    for it in range(3):
+        la = a.step(planes, tpol, tval, A.get_cyclical_lr(it))
+        lb = b.step(planes, tpol, tval, A.get_cyclical_lr(it))
+        assert la == lb
+    assert np.array_equal(a.params(), b.params())
+    assert np.array_equal(a.grads(), b.grads())
+
+
+def test_training_reduces_the_loss(require_gpu):
+    blocks, filters = 2, 32
+    tr = A.Trainer(blocks, filters, max_batch=32)
+    planes, tpol, tval = batch(32, seed=9)
+    first = sum(tr.step(planes, tpol, tval, 1e-3))
+    for _ in range(20):
+        last = sum(tr.step(planes, tpol, tval, 1e-3))
+    assert last < 0.8 * first, (first, last)
+    # the trained weights drive the inference engine (model.valid(), training.rs:83)
+    net = tr.model(dtype="f32")
+    pol, val = net.forward(planes[:4])
+    assert np.allclose(pol.sum(1), 1.0, atol=1e-4) and np.all(np.abs(val) <= 1)
