@@ -7,11 +7,12 @@ from . import _lib, parameters
 from .agent import AlphaZero, num_params, random_weights
 from .chess import (GameResult, GameState, IllegalMove, Position, index_to_move, move_to_index, play_move,
                     to_tensor)
+from .memory import ReplayBuffer, TrainingSample
 from .training import (EpisodeStep, SelfPlay, Trainer, comm_unique_id, get_cyclical_lr, process_batch,
-                       run_all_episodes, run_episode)
+                       run_all_episodes, run_episode, train)
 from .tree import BatchedSearch, MCTree, make_cfg
 
 __all__ = ["AlphaZero", "num_params", "random_weights", "GameResult", "GameState", "IllegalMove", "Position",
            "index_to_move", "move_to_index", "play_move", "to_tensor", "EpisodeStep", "SelfPlay", "Trainer", "comm_unique_id",
-           "get_cyclical_lr", "process_batch",
+           "get_cyclical_lr", "process_batch", "train", "ReplayBuffer", "TrainingSample",
            "run_all_episodes", "run_episode", "BatchedSearch", "MCTree", "make_cfg", "parameters"]

@@ -109,7 +109,17 @@ SIGNATURES = [
     ("az_trainer_get_params", C.c_int, [C.c_void_p, P(C.c_float), C.c_size_t]),
     ("az_trainer_get_grads", C.c_int, [C.c_void_p, P(C.c_float), C.c_size_t]),
     ("az_trainer_relu_output", C.c_int, [C.c_void_p, C.c_int, P(C.c_float), C.c_size_t]),
+    ("az_trainer_timing", C.c_int, [C.c_void_p, P(C.c_double), P(C.c_double), P(C.c_int64), C.c_int]),
     ("az_comm_unique_id", C.c_int, [C.c_void_p, C.c_int]),
+    ("az_replay_create", C.c_int, [C.c_int, P(C.c_void_p)]),
+    ("az_replay_destroy", C.c_int, [C.c_void_p]),
+    ("az_replay_len", C.c_int, [C.c_void_p]),
+    ("az_replay_add", C.c_int, [C.c_void_p, P(AzEpisodeStep)]),
+    ("az_replay_add_dense", C.c_int, [C.c_void_p, P(AzPos), P(C.c_float), C.c_float]),
+    ("az_replay_sample", C.c_int, [C.c_void_p, C.c_int, C.c_uint64, P(C.c_float), P(C.c_float), P(C.c_float),
+                                   P(AzPos)]),
+    ("az_replay_save", C.c_int, [C.c_void_p, C.c_char_p]),
+    ("az_replay_load", C.c_int, [C.c_char_p, C.c_int, P(C.c_void_p)]),
     ("az_trainer_set_comm", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int]),
 ]
 

@@ -13,6 +13,8 @@ import numpy as np
 
 from . import _lib as L
 from .chess import Position, to_tensor
+from .parameters import (BATCH_SIZE, MIN_REPLAY_SIZE, NUM_EPISODES, NUM_FILTERS, NUM_RES_BLOCKS, NUM_SIMULATIONS,
+                         NUM_TRAIN_STEPS, SEED)
 from .tree import BatchedSearch
 
 
@@ -57,11 +59,16 @@ class SelfPlay:
         return fin.value, act.value
 
     def drain(self):
+        return [_convert(s) for s in self.drain_raw()]
+
+    def drain_raw(self):
+        """EpisodeSteps of the games that ended, as the engine's az_episode_step records (what
+        ReplayBuffer.add takes directly)."""
         out = []
-        buf = (L.AzEpisodeStep * 4096)()
         while True:
+            buf = (L.AzEpisodeStep * 4096)()
             n = L.check(L.lib.az_selfplay_drain(self.search._h, buf, 4096))
-            out += [_convert(buf[i]) for i in range(n)]
+            out += [buf[i] for i in range(n)]
             if n < 4096:
                 return out
 
@@ -189,7 +196,62 @@ class Trainer:
         buf = (C.c_char * 128).from_buffer_copy(unique_id)
         L.check(L.lib.az_trainer_set_comm(self._h, buf, int(rank), int(world)))
 
+    def timing(self, reset=False):
+        """(step_ms, allreduce_ms, steps): device time summed over the steps since the last reset."""
+        a, b, n = C.c_double(), C.c_double(), C.c_int64()
+        L.check(L.lib.az_trainer_timing(self._h, C.byref(a), C.byref(b), C.byref(n), int(reset)))
+        return a.value, b.value, n.value
+
     def model(self, dtype="bf16"):
         """model.valid() for self-play (training.rs:83): an inference net with the current weights."""
         from .agent import AlphaZero
         return AlphaZero(self.blocks, self.filters, weights=self.params(), dtype=dtype, device=self.device)
+
+
+def train(iterations, blocks=NUM_RES_BLOCKS, filters=NUM_FILTERS, games=NUM_EPISODES, sims=NUM_SIMULATIONS,
+          min_replay=MIN_REPLAY_SIZE, train_steps=NUM_TRAIN_STEPS, batch_size=BATCH_SIZE, replay=None, trainer=None,
+          device=0, seed=SEED, dtype="bf16", comm=None, log=None):
+    """train() (training.rs:39-275) without the TUI, arena and Elo (SKIP_VALIDATION = true,
+    parameters.rs:35): per iteration, self-play `games` games with model.valid() until the replay
+    buffer holds min_replay unique positions, then train_steps AdamW steps on batches of
+    batch_size at get_cyclical_lr(iteration); the new model replaces the old one.
+    comm = (unique_id, rank, world) makes the gradient step data-parallel over RCCL: every rank
+    plays its own games (seed offset by rank) into its own buffer.
+    Returns (trainer, replay, per-iteration stats)."""
+    from .memory import ReplayBuffer
+    rank = comm[1] if comm else 0
+    if trainer is None:
+        trainer = Trainer(blocks, filters, max_batch=batch_size, device=device, seed=seed)
+        if comm:
+            trainer.set_comm(*comm)
+    replay = replay if replay is not None else ReplayBuffer()
+    history = []
+    for iteration in range(iterations):
+        model = trainer.model(dtype)
+        new_unique, plays = 0, 0
+        while True:
+            sp = SelfPlay(model, games=games, sims=sims, device=device, continuous=False,
+                          seed=seed + 1000003 * rank + 7919 * iteration + 104729 * plays)
+            sp.reset()
+            while True:
+                _, active = sp.step()
+                for st in sp.drain_raw():
+                    new_unique += replay.add(st)
+                if active == 0:
+                    break
+            plays += 1
+            if len(replay) >= min_replay:
+                break
+        lr = get_cyclical_lr(iteration)
+        pl_sum = vl_sum = 0.0
+        for b in range(train_steps):
+            planes, pol, val, _ = replay.sample_arrays(batch_size, seed=(seed << 20) ^ (iteration << 8) ^ b ^ rank << 40)
+            pl, vl = trainer.step(planes, pol, val, lr)
+            pl_sum += pl
+            vl_sum += vl
+        st = {"iteration": iteration, "replay": len(replay), "new_unique": new_unique, "lr": lr,
+              "policy_loss": pl_sum / max(train_steps, 1), "value_loss": vl_sum / max(train_steps, 1)}
+        history.append(st)
+        if log:
+            log(st)
+    return trainer, replay, history

@@ -548,6 +548,10 @@ struct Trainer {
     int rank = 0, world = 1;
     uint32_t* stat_idx = nullptr; float* stat_buf = nullptr; int nstat = 0;
     std::vector<void*> allocs;
+    // timing (HIP events on the trainer stream): whole steps and the gradient all-reduce
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    double step_ms = 0.0, allreduce_ms = 0.0;
+    long long steps_timed = 0;
 
     float* alloc(size_t n) {
         void* q = nullptr;
@@ -556,6 +560,7 @@ struct Trainer {
         return reinterpret_cast<float*>(q);
     }
     ~Trainer() {
+        for (hipEvent_t e : ev) if (e) (void)hipEventDestroy(e);
         if (comm) ncclCommDestroy(comm);
         for (void* q : allocs) (void)hipFree(q);
         if (hloss) (void)hipHostFree(hloss);
@@ -647,6 +652,7 @@ int trainer_grads(Trainer* T, const float* planes, const float* tpol, const floa
     if (B < 1 || B > T->Bmax) return fail("train: batch size out of range");
     T->last_batch = B;
     AZ_HIP(hipSetDevice(T->device));
+    AZ_HIP(hipEventRecord(T->ev[0], T->st));
     const int F = T->F, R = B * 64;
     hipStream_t st = T->st;
     const Layout& L = T->L;
@@ -773,24 +779,34 @@ float powi_f32(float x, long long n) {   // Rust f32::powi (repeated squaring in
 int trainer_apply(Trainer* T, double lr) {
     AZ_HIP(hipSetDevice(T->device));
     hipStream_t st = T->st;
-    if (T->comm && T->world > 1) {
+    AZ_HIP(hipEventRecord(T->ev[1], st));
+    if (T->comm) {   // a 1-rank communicator sums over itself: the identity, through RCCL
         if (ncclAllReduce(T->g, T->g, T->np, ncclFloat, ncclSum, T->comm, st) != ncclSuccess)
             return fail("ncclAllReduce (gradients) failed");
     }
+    AZ_HIP(hipEventRecord(T->ev[2], st));
     T->t++;
     const float bc1 = 1.0f - powi_f32(0.9f, T->t), bc2 = 1.0f - powi_f32(0.999f, T->t);
     const float decay_mul = (float)(1.0 - lr * 1e-4);   // WEIGHT_DECAY, parameters.rs:25
     tr::adamw_kernel<<<grid_for(T->np), 256, 0, st>>>(T->p, T->g, T->m, T->v, T->mask, T->np, 1.0f / (float)T->world,
                                                        decay_mul, (float)lr, bc1, bc2);
-    if (T->comm && T->world > 1) {   // average the BatchNorm running statistics over ranks
+    if (T->comm) {   // average the BatchNorm running statistics over ranks
         tr::stats_pack_kernel<<<grid_for(T->nstat), 256, 0, st>>>(T->p, T->stat_idx, T->nstat, T->stat_buf, 0, 1.0f);
         if (ncclAllReduce(T->stat_buf, T->stat_buf, T->nstat, ncclFloat, ncclSum, T->comm, st) != ncclSuccess)
             return fail("ncclAllReduce (running statistics) failed");
         tr::stats_pack_kernel<<<grid_for(T->nstat), 256, 0, st>>>(T->p, T->stat_idx, T->nstat, T->stat_buf, 1,
                                                                   1.0f / (float)T->world);
     }
+    AZ_HIP(hipEventRecord(T->ev[3], st));
     AZ_HIP(hipGetLastError());
     AZ_HIP(hipStreamSynchronize(st));
+    float a = 0.0f, b = 0.0f;
+    if (hipEventElapsedTime(&a, T->ev[0], T->ev[3]) == hipSuccess &&
+        hipEventElapsedTime(&b, T->ev[1], T->ev[2]) == hipSuccess) {
+        T->step_ms += a;
+        T->allreduce_ms += b;
+        T->steps_timed++;
+    }
     return 0;
 }
 
@@ -826,6 +842,7 @@ int az_trainer_create(int blocks, int filters, const float* weights, size_t n, i
     const int F = filters;
     const size_t R = (size_t)max_batch * 64;
     bool ok = hipStreamCreateWithFlags(&T->st, hipStreamNonBlocking) == hipSuccess;
+    for (hipEvent_t& e : T->ev) ok = ok && hipEventCreate(&e) == hipSuccess;
     auto A = [&](size_t k) { float* q = T->alloc(k); ok = ok && q; return q; };
     T->p = A(T->np); T->g = A(T->np); T->m = A(T->np); T->v = A(T->np);
     void* mk = nullptr;
@@ -956,6 +973,16 @@ int az_trainer_relu_output(az_trainer* t, int layer, float* out, size_t n) {
     AZ_HIP(hipSetDevice(T->device));
     AZ_HIP(hipStreamSynchronize(T->st));
     AZ_HIP(hipMemcpy(out, src, cnt * sizeof(float), hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int az_trainer_timing(az_trainer* t, double* step_ms, double* allreduce_ms, int64_t* steps, int reset) {
+    if (!t) return fail("null");
+    Trainer* T = t->t;
+    if (step_ms) *step_ms = T->step_ms;
+    if (allreduce_ms) *allreduce_ms = T->allreduce_ms;
+    if (steps) *steps = T->steps_timed;
+    if (reset) { T->step_ms = T->allreduce_ms = 0.0; T->steps_timed = 0; }
     return 0;
 }
 

@@ -60,6 +60,97 @@ def cpu_baseline(blocks, filters, threads, games, sims):
             "evals": nevals}
 
 
+def train_child(a):
+    """`bench.py --train-child ...`: the training step (training.rs:147-190) on
+    this rank's GPU, data-parallel over RCCL when world > 1 (gradients all-reduced over xGMI).
+    Synthetic batch of BATCH_SIZE (512) positions per rank: random-playout planes, sparse visit
+    policies, values in [-1, 1].  Prints one JSON line."""
+    import numpy as np
+    import azchess as A
+    rng = np.random.default_rng(1234 + a.rank)
+    B = a.train_batch
+    planes = np.zeros((B, 19, 64), np.float32)
+    for i in range(B):                         # piece-like one-hot planes + constant planes
+        sq = rng.permutation(64)[:int(rng.integers(4, 32))]
+        planes[i, rng.integers(0, 12, len(sq)), sq] = 1.0
+        planes[i, 12:16] = rng.integers(0, 2, (4, 1))
+        planes[i, 17] = rng.integers(0, 100) / 100.0
+        planes[i, 18] = rng.integers(1, 200) / 200.0
+    pol = np.zeros((B, 4096), np.float32)
+    for i in range(B):
+        idx = rng.choice(4096, 30, replace=False)
+        v = rng.integers(1, 40, 30).astype(np.float32)
+        pol[i, idx] = v / v.sum()
+    val = rng.uniform(-1, 1, B).astype(np.float32)
+    tr = A.Trainer(a.blocks, a.filters, max_batch=B, device=a.device, seed=42)
+    if a.world > 1:
+        tr.set_comm(bytes.fromhex(a.uid), a.rank, a.world)
+    for it in range(2):
+        tr.step(planes, pol, val, A.get_cyclical_lr(it))
+    tr.timing(reset=True)
+    t0 = time.perf_counter()
+    for it in range(a.train_steps):
+        tr.step(planes, pol, val, A.get_cyclical_lr(it))
+    wall = (time.perf_counter() - t0) / a.train_steps
+    dev_ms, ar_ms, n = tr.timing()
+    print(json.dumps({"ms_per_step": wall * 1e3, "device_ms_per_step": dev_ms / n, "allreduce_ms_per_step": ar_ms / n}))
+
+
+def train_phase(args, A, rank, world, local):
+    """Run train_child on every rank (subprocess with a time limit, so a collective that never
+    completes cannot hold the self-play measurement hostage); rank 0 returns the summary."""
+    import subprocess
+    uid = ""
+    if world > 1:
+        import torch.distributed as dist
+        box = [A.comm_unique_id().hex() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        uid = box[0]
+    cmd = [sys.executable, os.path.abspath(__file__), "--train-child", "--rank", str(rank), "--world", str(world),
+           "--device", str(local), "--uid", uid or "-", "--blocks", str(args.blocks), "--filters", str(args.filters),
+           "--train-steps", str(args.train_steps), "--train-batch", str(args.train_batch)]
+    res, err = None, None
+    try:
+        out = subprocess.run(cmd, capture_output=True, text=True, timeout=args.train_timeout)
+        lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+        if out.returncode == 0 and lines:
+            res = json.loads(lines[-1])
+        else:
+            err = "rc %d: %s" % (out.returncode, (out.stderr or out.stdout)[-400:])
+    except subprocess.TimeoutExpired:
+        err = "timed out after %d s" % args.train_timeout
+    ms = res["ms_per_step"] if res else float("nan")
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        t = torch.tensor([ms if res else float("inf")], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms = float(t.item())
+    if rank != 0:
+        return None
+    flop = 3.0 * net_flop_per_eval(args.blocks, args.filters) * args.train_batch
+    out = {"what": "training.rs:147-190 step: training-mode forward + backward + clip + AdamW, f32 "
+                   "(v_mfma_f32_16x16x4_f32), %d positions per rank%s" %
+                   (args.train_batch, ", gradients all-reduced over RCCL" if world > 1 else ""),
+           "global_batch": args.train_batch * world, "dtype": "f32"}
+    if res and ms == ms and ms != float("inf"):
+        tf = flop / (res["device_ms_per_step"] * 1e-3) / 1e12
+        out.update({"ms_per_step": ms, "samples_per_s": args.train_batch * world / (ms * 1e-3),
+                    "device_ms_per_step": res["device_ms_per_step"],
+                    "allreduce_ms_per_step": res["allreduce_ms_per_step"],
+                    "allreduce_bytes": 4 * int(A._lib.lib.az_net_num_params(args.blocks, args.filters)),
+                    "achieved_tflops": tf, "peak_tflops": PEAK_F32_TFLOPS, "frac": tf / PEAK_F32_TFLOPS,
+                    "flop_per_step": flop})
+    else:
+        out["error"] = err or "a rank failed"
+    return out
+
+
+def net_flop_per_eval(B, F):
+    """forward FLOPs per position"""
+    return 2.0 * 64.0 * (171.0 * F + 18.0 * B * F * F + 40.0 * F + 2048.0) + 2.0 * (32768.0 + 64.0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -75,7 +166,17 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-games", type=int, default=16)
     ap.add_argument("--cpu-sims", type=int, default=8)
+    ap.add_argument("--train-steps", type=int, default=5, help="timed training steps (0 = skip the training phase)")
+    ap.add_argument("--train-batch", type=int, default=512, help="positions per rank (BATCH_SIZE, parameters.rs:17)")
+    ap.add_argument("--train-timeout", type=int, default=240)
+    ap.add_argument("--train-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--rank", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--world", type=int, default=1, help=argparse.SUPPRESS)
+    ap.add_argument("--device", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--uid", default="-", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.train_child:
+        return train_child(args)
 
     # libaz (and the /opt/rocm HIP runtime it is built for) is loaded before torch: torch
     # bundles its own libamdhip64.so.7 (same SONAME) and is only used here for the gloo
@@ -144,6 +245,7 @@ def main():
                      "note": "same window with the reference's FEN evaluation cache (A12); games are in "
                              "lockstep from startpos, so early moves share most positions"}
 
+    training = train_phase(args, A, rank, world, local) if args.train_steps > 0 else None
     if rank != 0:
         dist.destroy_process_group()
         return
@@ -198,6 +300,7 @@ def main():
         "games_finished": int(fin_all),
         "games_per_hr": fin_all / elapsed * 3600.0,
         "cpu_baseline": None,
+        "training": training,
     }
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.blocks, args.filters, args.cpu_threads, args.cpu_games,

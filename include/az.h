@@ -214,10 +214,31 @@ int az_trainer_get_grads(az_trainer* t, float* out, size_t n);
  * [B*64][F]), 2B+1 = head convs after BN+ReLU [B*64][64] (columns 0..39), 2B+2 =
  * value_linear_1 output before its ReLU [B][64].  n must equal the tensor's size. */
 int az_trainer_relu_output(az_trainer* t, int layer, float* out, size_t n);
+/* device time (HIP events on the trainer stream) summed over steps: whole step (compute_grads
+ * start to apply end) and the gradient all-reduce; reset = zero the sums after reading */
+int az_trainer_timing(az_trainer* t, double* step_ms, double* allreduce_ms, int64_t* steps, int reset);
 /* data-parallel training over RCCL (xGMI): rank 0 creates the id (128 bytes, returns its
  * size), every rank passes it to az_trainer_set_comm. */
 int az_comm_unique_id(void* out, int cap);
 int az_trainer_set_comm(az_trainer* t, const void* unique_id, int rank, int world);
+
+/* ---- replay buffer: memory.rs ReplayBuffer, host memory ------------ */
+typedef struct az_replay az_replay;
+int az_replay_create(int capacity, az_replay** out);                /* ReplayBuffer::new, memory.rs:33-38 */
+int az_replay_destroy(az_replay* r);
+int az_replay_len(const az_replay* r);                              /* memory.rs:103-105 */
+/* ReplayBuffer::add (memory.rs:41-79): running mean into an existing FEN entry (returns 0) or
+ * a new entry at the FIFO's end, evicting the oldest at capacity (returns 1) */
+int az_replay_add(az_replay* r, const az_episode_step* step);
+int az_replay_add_dense(az_replay* r, const az_pos* state, const float* policy, float value);
+/* ReplayBuffer::sample (memory.rs:81-101): min(batch, len) distinct entries, uniformly (seeded);
+ * writes to_tensor planes [n,19,64], policies [n,4096], values [n], positions (any may be NULL).
+ * Returns n. */
+int az_replay_sample(az_replay* r, int batch, uint64_t seed, float* planes, float* policy, float* value,
+                     az_pos* states);
+/* save / load (memory.rs:107-117): bincode 2 standard-config file of the reference's layout */
+int az_replay_save(const az_replay* r, const char* path);
+int az_replay_load(const char* path, int capacity, az_replay** out);
 
 #ifdef __cplusplus
 }

@@ -141,3 +141,15 @@ def test_training_reduces_the_loss(require_gpu):
     net = tr.model(dtype="f32")
     pol, val = net.forward(planes[:4])
     assert np.allclose(pol.sum(1), 1.0, atol=1e-4) and np.all(np.abs(val) <= 1)
+
+
+def test_full_loop_selfplay_replay_train(require_gpu):
+    """training.rs train(): self-play -> memory.rs replay -> training steps -> new model, twice."""
+    logs = []
+    tr, replay, hist = A.train(2, blocks=2, filters=32, games=16, sims=8, min_replay=200, train_steps=3,
+                               batch_size=64, dtype="f32", log=logs.append)
+    assert len(hist) == 2 and len(replay) >= 200
+    assert all(np.isfinite(h["policy_loss"]) and np.isfinite(h["value_loss"]) for h in hist)
+    assert hist[1]["lr"] == A.get_cyclical_lr(1)
+    step_ms, ar_ms, n = tr.timing()
+    assert n == 6 and step_ms > 0 and ar_ms < 1.0
