@@ -4,7 +4,7 @@ Host-side mirror of the reference's module surface (chess.rs, agent.rs, tree.rs,
 training.rs, parameters.rs) over the C-ABI of libaz.so (include/az.h).
 """
 from . import _lib, parameters
-from .agent import AlphaZero, num_params, random_weights
+from .agent import AlphaZero, load_model, load_mpk, num_params, random_weights, save_mpk
 from .chess import (GameResult, GameState, IllegalMove, Position, index_to_move, move_to_index, play_move,
                     to_tensor)
 from .memory import ReplayBuffer, TrainingSample
@@ -12,7 +12,7 @@ from .training import (EpisodeStep, SelfPlay, Trainer, comm_unique_id, get_cycli
                        run_all_episodes, run_episode, train)
 from .tree import BatchedSearch, MCTree, make_cfg
 
-__all__ = ["AlphaZero", "num_params", "random_weights", "GameResult", "GameState", "IllegalMove", "Position",
+__all__ = ["AlphaZero", "load_model", "load_mpk", "save_mpk", "num_params", "random_weights", "GameResult", "GameState", "IllegalMove", "Position",
            "index_to_move", "move_to_index", "play_move", "to_tensor", "EpisodeStep", "SelfPlay", "Trainer", "comm_unique_id",
            "get_cyclical_lr", "process_batch", "train", "ReplayBuffer", "TrainingSample",
            "run_all_episodes", "run_episode", "BatchedSearch", "MCTree", "make_cfg", "parameters"]

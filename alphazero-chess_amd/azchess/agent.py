@@ -57,6 +57,25 @@ def random_weights(blocks=NUM_RES_BLOCKS, filters=NUM_FILTERS, seed=SEED, bn_per
     return flat
 
 
+def load_mpk(path, blocks=NUM_RES_BLOCKS, filters=NUM_FILTERS):
+    """NamedMpkFileRecorder::<FullPrecisionSettings>::new().load(path) (main.rs:109-116):
+    the record's tensors in the flat layout of include/az.h."""
+    out = np.empty(num_params(blocks, filters), np.float32)
+    L.check(L.lib.az_net_load_mpk(str(path).encode(), int(blocks), int(filters), L.fptr(out), out.size))
+    return out
+
+
+def save_mpk(path, weights, blocks=NUM_RES_BLOCKS, filters=NUM_FILTERS):
+    """model.save_file(path, &NamedMpkFileRecorder::<FullPrecisionSettings>) (training.rs:269-270)."""
+    w = np.ascontiguousarray(weights, np.float32)
+    L.check(L.lib.az_net_save_mpk(str(path).encode(), int(blocks), int(filters), L.fptr(w), w.size))
+
+
+def load_model(path, blocks=NUM_RES_BLOCKS, filters=NUM_FILTERS, dtype="bf16", device=0):
+    """main.rs:109-116: AlphaZero::new().load_record(record)."""
+    return AlphaZero(blocks, filters, weights=load_mpk(path, blocks, filters), dtype=dtype, device=device)
+
+
 class AlphaZero:
     """AlphaZero::new / forward (agent.rs:49-144) with weights resident in HBM."""
 
@@ -79,6 +98,9 @@ class AlphaZero:
             L.lib.az_net_destroy(self._h)
         except Exception:
             pass
+
+    def save_file(self, path):
+        save_mpk(path, self.weights, self.blocks, self.filters)
 
     def forward(self, x):
         """x: [N,19,8,8] float32 -> (policy [N,4096] softmax, value [N] tanh)."""

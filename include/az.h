@@ -86,6 +86,11 @@ size_t az_net_num_params(int blocks, int filters);
  * BatchNorm folded into the convs (inference mode, model.valid()). */
 int az_net_create(const az_net_desc* desc, const float* weights, size_t n, int device, az_net** out);
 int az_net_destroy(az_net* net);
+/* burn NamedMpkFileRecorder<FullPrecisionSettings> model files:
+ * load_model (main.rs:109-116) -> flat weights for az_net_create / az_trainer_create, and
+ * model.save_file (training.rs:269-270) from flat weights.  out/w hold az_net_num_params floats. */
+int az_net_load_mpk(const char* path, int blocks, int filters, float* out, size_t n);
+int az_net_save_mpk(const char* path, int blocks, int filters, const float* w, size_t n);
 /* AlphaZero::forward (agent.rs:112-144): planes [n,19,8,8] f32 -> policy [n,4096]
  * (softmax) and value [n] (tanh). Host buffers. */
 int az_net_forward(az_net* net, const float* planes, int n, float* policy, float* value);

@@ -96,3 +96,15 @@ def test_fused_tower_matches_per_layer_kernels(require_gpu, blocks, filters, mon
     # occasional bf16 rounding flips -> bf16-scale tolerance (each path is also checked vs the oracle)
     np.testing.assert_allclose(vf, vl, atol=2e-3)
     np.testing.assert_allclose(pf, pl, rtol=2e-2, atol=1e-6)
+
+
+def test_mpk_model_file_drives_the_engine(require_gpu, tmp_path):
+    """model.save_file -> load_model (training.rs:269-270, main.rs:109-116) -> identical outputs."""
+    w = A.random_weights(2, 32, seed=12)
+    net = A.AlphaZero(2, 32, weights=w, dtype="f32")
+    p = tmp_path / "iteration_3_elo_0.mpk"
+    net.save_file(p)
+    back = A.load_model(p, 2, 32, dtype="f32")
+    x = np.stack([A.to_tensor(A.Position.startpos())[0]] * 3)
+    a, b = net.forward(x), back.forward(x)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
