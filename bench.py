@@ -29,6 +29,9 @@ PEAK_HBM_GBS = 8000.0         # MI355X_MICROARCH.md: 8.0 TB/s spec
 # HBM bytes per tower launch from rocprofv3 PMC passes (tools/pmc_run.sh: FETCH_SIZE x2 per the
 # gfx950 correction + WRITE_SIZE), same kernel and per-launch work (2048 rows, 20x256 bf16)
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_tower_summary.json")
+# mean plies of complete self-play games of this config (tools/game_length.py: 256 games, 20x256
+# random-init seed 42, 800 sims/move, noise + temperature moves, played to the end)
+GAME_LENGTH = os.path.join(ROOT, "profiles", "r01_game_length_256.json")
 
 
 def pmc_traffic(games, blocks, filters, dtype):
@@ -299,9 +302,20 @@ def main():
         "avg_search_depth": depth_all / max(moves_all, 1),
         "games_finished": int(fin_all),
         "games_per_hr": fin_all / elapsed * 3600.0,
+        "games_per_hr_projected": None,
         "cpu_baseline": None,
         "training": training,
     }
+    if (args.blocks, args.filters, S) == (20, 256, 800) and os.path.exists(GAME_LENGTH):
+        with open(GAME_LENGTH) as f:
+            gl = json.load(f)
+        # continuous self-play keeps every slot busy (a finished game restarts in its slot), so
+        # the steady state plays sims/s / (sims/move * plies/game) games
+        out["games_per_hr_projected"] = {
+            "value": value * 3600.0 / (S * gl["plies_mean"]), "plies_per_game": gl["plies_mean"],
+            "source": os.path.relpath(GAME_LENGTH, ROOT),
+            "note": "steady-state continuous self-play: measured sims/s / (800 sims x mean plies of %d complete "
+                    "games); the timed window is %d moves, too short for games to finish" % (gl["games"], args.steps)}
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.blocks, args.filters, args.cpu_threads, args.cpu_games,
                                            args.cpu_sims)
