@@ -19,6 +19,7 @@ TEMPERATURE_ANNEALING = 15         # parameters.rs:31
 NUM_SIMULATIONS = 256              # parameters.rs:32
 TEMPERATURE = 1.0                  # parameters.rs:33 (only T = 1 is supported: visits^(1/T) = visits)
 C_PUCT = 3.0                       # parameters.rs:34
+EVALUATION_GAMES = 256             # parameters.rs:36
 NUM_HALFMOVES = 100                # chess.rs:9
 NUM_FULLMOVES = 200                # chess.rs:10
 REPETITIONS = 3                    # chess.rs:11
