@@ -108,6 +108,7 @@ struct NetDev {
     std::vector<void*> conv_w;      // swizzled MFMA fragments per conv (1 + 2*blocks)
     std::vector<float*> conv_b;     // folded bias per conv
     float* head = nullptr;          // folded head weights (f32)
+    void* head_frag = nullptr;      // 1x1 F->40 head conv as bf16 hi/lo MFMA A-fragments (fused tower)
     size_t head_floats = 0;
     hipStream_t stream = nullptr;
     bool fused = true;              // use tower_forward when supported (AZ_FUSED_TOWER=0 disables)

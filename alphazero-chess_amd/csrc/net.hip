@@ -504,6 +504,33 @@ int net_create(const az_net_desc* d, const float* wts, size_t n, int device, Net
     net->head_floats = L.total;
     AZ_HIP(hipMalloc(&net->head, L.total * 4));
     AZ_HIP(hipMemcpy(net->head, hw.data(), L.total * 4, hipMemcpyHostToDevice));
+    {
+        // the fused tower's heads run the 1x1 F->40 conv on bf16 MFMA with each f32 weight split
+        // into hi = bf16(w) and lo = bf16(w - hi): [ks F/32][cf 3 (40 -> 48 rows)][hi, lo][lane][8],
+        // lane = A-fragment row (co = cf*16 + lane%16) x k (ci = ks*32 + 8*(lane/16) + j)
+        std::vector<uint16_t> fr((size_t)(F / 32) * 3 * 2 * 64 * 8, 0);
+        auto bf = [](float v) {
+            uint32_t u;
+            memcpy(&u, &v, 4);
+            return (uint16_t)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+        };
+        for (int ks = 0; ks < F / 32; ks++)
+            for (int cf = 0; cf < 3; cf++)
+                for (int lane = 0; lane < 64; lane++)
+                    for (int j = 0; j < 8; j++) {
+                        const int co = cf * 16 + (lane & 15), ci = ks * 32 + 8 * (lane >> 4) + j;
+                        const float v = co < 40 ? hw[L.w40 + (size_t)co * F + ci] : 0.0f;
+                        const uint16_t hi = bf(v);
+                        const uint32_t hu = (uint32_t)hi << 16;
+                        float hf;
+                        memcpy(&hf, &hu, 4);
+                        const size_t o = ((((size_t)ks * 3 + cf) * 2) * 64 + lane) * 8 + j;
+                        fr[o] = hi;
+                        fr[o + 64 * 8] = bf(v - hf);
+                    }
+        AZ_HIP(hipMalloc(&net->head_frag, fr.size() * 2));
+        AZ_HIP(hipMemcpy(net->head_frag, fr.data(), fr.size() * 2, hipMemcpyHostToDevice));
+    }
     *out = net;
     return 0;
 }
@@ -514,6 +541,7 @@ void net_destroy(NetDev* n) {
     for (void* w : n->conv_w) (void)hipFree(w);
     for (float* b : n->conv_b) (void)hipFree(b);
     (void)hipFree(n->head);
+    (void)hipFree(n->head_frag);
     (void)hipFree(n->x); (void)hipFree(n->h); (void)hipFree(n->planes);
     (void)hipFree(n->d_in); (void)hipFree(n->d_pol); (void)hipFree(n->d_val);
     if (n->stream) (void)hipStreamDestroy(n->stream);

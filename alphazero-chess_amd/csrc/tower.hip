@@ -11,6 +11,8 @@
 // The heads run from the same LDS image (f32 VALU), in dense mode (policy[4096],
 // value) or in search mode (softmax gathered at the new node's legal edges).
 #include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "az_internal.h"
@@ -20,6 +22,14 @@
 #endif
 #ifndef AZ_TOWER_NCO256
 #define AZ_TOWER_NCO256 2
+#endif
+#ifndef AZ_TOWER_PRIO
+#define AZ_TOWER_PRIO 0    // the two waves sharing a SIMD (w, w+4) take turns at issue priority, per
+                           // PRIO k-steps: without it the older wave races ahead and the other
+                           // finishes its layer alone, latency-bound (0 = off)
+#endif
+#ifndef AZ_TOWER_LA
+#define AZ_TOWER_LA 4      // activation (B-fragment) LDS reads issued this many fragments ahead
 #endif
 #ifndef AZ_TOWER_PF
 #define AZ_TOWER_PF 2      // weight prefetch depth in k-steps (L2 latency cover; 4 measured no faster)
@@ -35,8 +45,21 @@ struct TowerArgs {
     const uint4* w[1 + 2 * 40];    // swizzled conv weights (input conv, then conv1/conv2 per block)
     const float* b[1 + 2 * 40];    // folded biases
     const float* head;
+    const uint4* head_frag;        // 1x1 F->40 head conv as bf16 hi/lo MFMA A-fragments (net.hip)
     int blocks;
+#ifdef AZ_TOWER_TRACE
+    unsigned long long* trace;     // experiment only: [grid][TR_SLOTS] s_memrealtime stamps (100 MHz)
+#endif
 };
+#ifdef AZ_TOWER_TRACE
+constexpr int TR_SLOTS = 128;
+#define TR_STAMP(k)                                                                                  \
+    do {                                                                                             \
+        if (tid == 0) ta.trace[(size_t)blockIdx.x * TR_SLOTS + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define TR_STAMP(k) do { } while (0)
+#endif
 
 // BPB boards per workgroup; NCO 16-channel output fragments per wave; WB board groups.
 // waves = (F / (16*NCO)) * WB
@@ -78,8 +101,9 @@ template <int CIN, int RSI, int F, int RSO, int BPW, int NCO, bool RESID>
 __device__ __forceinline__ void conv_lds(const char* __restrict__ ldsb, uint4* __restrict__ out_lds, int in_off,
                                          int zero_off, const uint4* __restrict__ wsw, const uint4* __restrict__ wnext,
                                          const float* __restrict__ bias, uint4 (&wr)[RingPF<CIN / 32>::PF][NCO],
-                                         int cw, int bw, int lane) {
+                                         int cw, int bw, int lane, int wpar, unsigned long long* trw = nullptr) {
     constexpr int NCH = CIN / 32;                     // 32-channel K chunks (4 slots)
+    if (trw && lane == 0) trw[0] = __builtin_amdgcn_s_memtime();
     constexpr int CF = F / 16;
     constexpr int MF = BPW * 4;
     constexpr int KS = 9 * NCH;
@@ -101,7 +125,7 @@ __device__ __forceinline__ void conv_lds(const char* __restrict__ ldsb, uint4* _
     const uint4* Wn = (wnext ? wnext + (size_t)(cw * NCO) * 64 + lane : W + (size_t)KS * CF * 64) - (size_t)KS * CF * 64;
     // B-fragment (activation) reads run LA fragments ahead, across k-step and tap boundaries:
     // the first LA reads of step s+1 are issued inside step s.
-    constexpr int LA = 4;
+    constexpr int LA = AZ_TOWER_LA < MF ? AZ_TOWER_LA : MF;
     static_assert(MF % LA == 0, "read-ahead ring must tile the fragment loop");
     auto tap_bases = [&](int tap, int* base) {
         const int dr = tap / 3 - 1, df = tap % 3 - 1;
@@ -125,13 +149,22 @@ __device__ __forceinline__ void conv_lds(const char* __restrict__ ldsb, uint4* _
 #pragma unroll
         for (int cc = 0; cc < NCH; cc++) {
             const int ks = tap * NCH + cc;
+            if constexpr (AZ_TOWER_PRIO > 0) {
+                if ((((cc / AZ_TOWER_PRIO) & 1) ^ wpar) != 0) __builtin_amdgcn_s_setprio(1);
+                else __builtin_amdgcn_s_setprio(0);
+            }
             uint4 a[NCO];
 #pragma unroll
             for (int n = 0; n < NCO; n++) a[n] = wr[cc % PF][n];
             // refill this ring slot with k-step ks+PF (of the next layer once past the end)
             const uint4* Wsrc = (tap == 8 && cc + PF >= NCH) ? Wn : W;
 #pragma unroll
+#ifdef AZ_TOWER_L1W   // experiment only: every k-step re-reads k-steps 0..1 (L1-resident weights)
+            for (int n = 0; n < NCO; n++) wr[cc % PF][n] = W[(size_t)((ks + PF) & 1) * CF * 64 + n * 64];
+            (void)Wsrc;
+#else
             for (int n = 0; n < NCO; n++) wr[cc % PF][n] = Wsrc[(size_t)(ks + PF) * CF * 64 + n * 64];
+#endif
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int m = 0; m < MF; m++) {
@@ -160,6 +193,8 @@ __device__ __forceinline__ void conv_lds(const char* __restrict__ ldsb, uint4* _
         for (int m = 0; m < MF; m++) bcur[m] = bnext[m];
     }
     (void)KS;
+    if constexpr (AZ_TOWER_PRIO > 0) __builtin_amdgcn_s_setprio(0);
+    if (trw && lane == 0) trw[1] = __builtin_amdgcn_s_memtime();
     // `in` and `out` are different buffers, so the epilogue needs no barrier before it;
     // the barrier after it publishes `out` to the next layer.
     char* ob = reinterpret_cast<char*>(out_lds);
@@ -189,116 +224,202 @@ __device__ __forceinline__ void conv_lds(const char* __restrict__ ldsb, uint4* _
             *dst = make_uint2(__builtin_bit_cast(unsigned, q0), __builtin_bit_cast(unsigned, q1));
         }
     }
+    if (trw && lane == 0) trw[2] = __builtin_amdgcn_s_memtime();
     __syncthreads();
+    if (trw && lane == 0) trw[3] = __builtin_amdgcn_s_memtime();
 }
 
-// heads for one board from the LDS image x (bf16, row stride RS slots); 256 threads (t < 256).
-template <int F, int RS, bool SEARCH>
-__device__ __forceinline__ void heads_lds(const char* __restrict__ xb, float* __restrict__ scratch, int t,
-                                          const float* __restrict__ head, bool writer, bool valid, int row,
-                                          float* pol_out, float* val_out, const SearchOut& so) {
-    // writer: this 256-thread group owns `scratch` (idle groups only join the barriers)
+// Heads v2 for NB boards [b0, b0 + NB) of the workgroup, from the LDS image x (bf16, row
+// stride RS slots), scratch in H; every one of the NT threads reaches every barrier.
+//   A: 1x1 F->40 (policy conv 32 + value conv 8, BN folded) on v_mfma_f32_16x16x32_bf16 with the
+//      f32 weights split into bf16 hi + lo fragments (16 mantissa bits; activations are bf16
+//      already), bias + ReLU -> p1v1 (f32);
+//   B: policy 1x1 32->64 on v_mfma_f32_16x16x4_f32 (exact f32 products) -> 4096 logits;
+//   C: value Linear 512->64 (K split over the waves), ReLU, Linear 64->1, tanh (f32 VALU);
+//   then softmax over 4096 and the dense rows or, in search mode, the priors gathered at the
+//   new node's legal edges (agent.rs:112-144, tree.rs:84-104).
+template <int F> struct HeadsCfg { static constexpr int NB = F >= 128 ? 2 : 1; };
+constexpr int HEADS_P1S = 80;                           // p1v1 row stride in floats (conflict-free B reads)
+template <int NB, int NT> struct HeadsScratch {
+    static constexpr int PV = 40 * HEADS_P1S, NW = NT / 64;
+    static constexpr int P1 = 0, LG = P1 + NB * PV, RED = LG + NB * 4096, STAT = RED + NB * NW * 64;
+    static constexpr int FLOATS = STAT + NB * (2 * NW + 4);
+};
+
+template <int F, int RS, int NB, int NT, bool SEARCH>
+__device__ __forceinline__ void heads_group(const char* __restrict__ xb, float* __restrict__ scr, int b0, int nb,
+                                            int row0, int tid, const uint4* __restrict__ hfrag,
+                                            const float* __restrict__ head, float* pol_out, float* val_out,
+                                            const SearchOut& so, unsigned long long* trh = nullptr) {
+    typedef HeadsScratch<NB, NT> S;
+    constexpr int NW = S::NW, PV = S::PV, P1S = HEADS_P1S;
     const HeadLayout L = HeadLayout::make(F);
-    float* p1 = scratch;                 // [32][64]
-    float* v1 = p1 + 32 * 64;            // [8][64]
-    float* lg = v1 + 8 * 64;             // [4096]
-    float* red = lg + 4096;              // [256]
-    float* stat = red + 256;             // [8]
-    const int sq = t & 63;
-    const int g = __builtin_amdgcn_readfirstlane(t >> 6);
-    if (valid) {
-        float acc[10];
+    const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), h = lane >> 4, l16 = lane & 15;
+    float* p1v1 = scr + S::P1;
+    float* lg = scr + S::LG;
+    float* red = scr + S::RED;
+    float* stat = scr + S::STAT;                        // per board: [NW] max, [NW] sum, value, slot, prior off
+    // weights of B and C are fetched into registers first: their latency hides behind A
+    constexpr int TPW = 16 * NB / NW;                   // policy tiles per wave
+    constexpr int KP = 512 / NW, KPRE = KP < 64 ? KP : 64;
+    float pa[TPW > 0 ? TPW : 1][8];
 #pragma unroll
-        for (int j = 0; j < 10; j++) acc[j] = 0.0f;
-        const float* w40 = head + L.w40 + (size_t)g * 10 * F;
-        const char* xr = xb + sq * RS * 16;
-        for (int c8 = 0; c8 < F / 8; c8++) {
-            const bf16x8 xv = *reinterpret_cast<const bf16x8*>(xr + c8 * 16);
+    for (int k = 0; k < TPW; k++) {
+        const int t = w + k * NW, cf = (t >> 2) & 3;
 #pragma unroll
-            for (int e = 0; e < 8; e++) {
-                const float x = (float)xv[e];
+        for (int ks = 0; ks < 8; ks++) pa[k][ks] = head[L.p2w + (cf * 16 + l16) * 32 + h + ks * 4];
+    }
+    float wv[KPRE];
 #pragma unroll
-                for (int j = 0; j < 10; j++) acc[j] += w40[j * F + c8 * 8 + e] * x;
+    for (int i = 0; i < KPRE; i++) wv[i] = head[L.l1w + (size_t)(w * KP + i) * 64 + lane];
+    // A
+    for (int sfr = w; sfr < 4 * NB; sfr += NW) {
+        const int bb = sfr >> 2, sq = (sfr & 3) * 16 + l16;
+        const char* xr = xb + ((size_t)(b0 + bb) * 64 + sq) * RS * 16 + h * 16;
+        f32x4 acc[3];
+#pragma unroll
+        for (int cf = 0; cf < 3; cf++) acc[cf] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int ks = 0; ks < F / 32; ks++) {
+            const bf16x8 Bv = *reinterpret_cast<const bf16x8*>(xr + ks * 64);
+#pragma unroll
+            for (int cf = 0; cf < 3; cf++)
+#pragma unroll
+                for (int hl = 0; hl < 2; hl++)
+                    acc[cf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        __builtin_bit_cast(bf16x8, hfrag[((ks * 3 + cf) * 2 + hl) * 64 + lane]), Bv, acc[cf], 0, 0, 0);
+        }
+#pragma unroll
+        for (int cf = 0; cf < 3; cf++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int ch = cf * 16 + 4 * h + r;
+                if (ch < 40) p1v1[bb * PV + ch * P1S + sq] = fmaxf(acc[cf][r] + head[L.b40 + ch], 0.0f);
+            }
+    }
+    __syncthreads();
+    if (trh && tid == 0) trh[0] = __builtin_amdgcn_s_memrealtime();
+    // B
+    float mxb[NB];
+#pragma unroll
+    for (int bb = 0; bb < NB; bb++) mxb[bb] = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < TPW; k++) {
+        const int t = w + k * NW;
+        const int bb = t >> 4, cf = (t >> 2) & 3, sf = t & 3;
+        const float* pb = p1v1 + bb * PV + h * P1S + sf * 16 + l16;
+        f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int ks = 0; ks < 8; ks++) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[k][ks], pb[ks * 4 * P1S], acc, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int c2 = cf * 16 + 4 * h + r;
+            const float l = acc[r] + head[L.p2b + c2];
+            lg[bb * 4096 + c2 * 64 + sf * 16 + l16] = l;
+#pragma unroll
+            for (int q = 0; q < NB; q++)
+                if (q == bb) mxb[q] = fmaxf(mxb[q], l);
+        }
+    }
+    // C: value FC, wave w owns K rows [w*KP, (w+1)*KP), lane = output unit
+    {
+        float a[NB];
+#pragma unroll
+        for (int bb = 0; bb < NB; bb++) a[bb] = 0.0f;
+#pragma unroll
+        for (int i = 0; i < KP; i++) {
+            const int k = w * KP + i, c = 32 + (k >> 6), sq = k & 63;
+            const float wgt = i < KPRE ? wv[i < KPRE ? i : 0] : head[L.l1w + (size_t)k * 64 + lane];
+#pragma unroll
+            for (int bb = 0; bb < NB; bb++) a[bb] += p1v1[bb * PV + c * P1S + sq] * wgt;
+        }
+#pragma unroll
+        for (int bb = 0; bb < NB; bb++) red[(bb * NW + w) * 64 + lane] = a[bb];
+    }
+#pragma unroll
+    for (int bb = 0; bb < NB; bb++) {
+        const float m = t_wave_max(mxb[bb]);
+        if (lane == 0) stat[bb * (2 * NW + 4) + w] = m;
+    }
+    __syncthreads();
+    float mx[NB];
+#pragma unroll
+    for (int bb = 0; bb < NB; bb++) {
+        float m = -INFINITY;
+        for (int i = 0; i < NW; i++) m = fmaxf(m, stat[bb * (2 * NW + 4) + i]);
+        mx[bb] = m;
+        float e = 0.0f;
+        for (int i = tid; i < 4096; i += NT) e += expf(lg[bb * 4096 + i] - m);
+        e = t_wave_sum(e);
+        if (lane == 0) stat[bb * (2 * NW + 4) + NW + w] = e;
+    }
+    if (w < NB) {                                       // wave bb finishes board bb's value head
+        const int bb = w;
+        float hs = head[L.l1b + lane];
+        for (int i = 0; i < NW; i++) hs += red[(bb * NW + i) * 64 + lane];
+        float hv = t_wave_sum(fmaxf(hs, 0.0f) * head[L.l2w + lane]);
+        if (lane == 0) stat[bb * (2 * NW + 4) + 2 * NW] = tanhf(hv + head[L.l2b]);
+    }
+    if (trh && tid == 0) trh[1] = __builtin_amdgcn_s_memrealtime();
+    if constexpr (SEARCH) {                             // thread 0 reserves eval-log slots
+        if (tid == 0 && so.log_cap > 0) {
+#pragma unroll
+            for (int bb = 0; bb < NB; bb++) {
+                int* sl = reinterpret_cast<int*>(stat + bb * (2 * NW + 4) + 2 * NW + 1);
+                sl[0] = -1;
+                if (b0 + bb >= nb) continue;
+                const int row = row0 + b0 + bb;
+                const int game = so.row_game[row], node = so.row_node[row];
+                const Node nd = so.nodes[(size_t)game * so.NMAX + node];
+                const int r = atomicAdd(&so.ctr->log_count, 1);
+                const int po = atomicAdd(&so.ctr->log_prior_count, (int)nd.nedges);
+                sl[0] = (r < so.log_cap && po + nd.nedges <= so.log_prior_cap) ? r : -1;
+                sl[1] = po;
             }
         }
+    }
+    __syncthreads();
+    if (trh && tid == 0) trh[2] = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
-        for (int j = 0; j < 10; j++) {
-            const int ch = g * 10 + j;
-            const float v = fmaxf(acc[j] + head[L.b40 + ch], 0.0f);
-            if (ch < 32) p1[ch * 64 + sq] = v; else v1[(ch - 32) * 64 + sq] = v;
-        }
-    }
-    __syncthreads();
-    float mx = -INFINITY;
-    if (valid) {
-#pragma unroll
-        for (int j = 0; j < 16; j++) {
-            const int c2 = g * 16 + j;
-            float l = 0.0f;
-            for (int c1 = 0; c1 < 32; c1++) l += head[L.p2w + c2 * 32 + c1] * p1[c1 * 64 + sq];
-            l += head[L.p2b + c2];
-            lg[c2 * 64 + sq] = l;
-            mx = fmaxf(mx, l);
-        }
-        const int o = t & 63;
-        float a = 0.0f;
-        for (int i = g * 128; i < g * 128 + 128; i++) a += v1[i] * head[L.l1w + i * 64 + o];
-        red[g * 64 + o] = a;
-    }
-    mx = t_wave_max(mx);
-    if (writer && (t & 63) == 0) stat[g] = mx;
-    __syncthreads();
-    mx = fmaxf(fmaxf(stat[0], stat[1]), fmaxf(stat[2], stat[3]));
-    float s = 0.0f;
-    if (valid)
-        for (int i = t; i < 4096; i += 256) s += expf(lg[i] - mx);
-    s = t_wave_sum(s);
-    float hv = 0.0f;
-    if (writer && t < 64) {
-        const float hsum = red[t] + red[64 + t] + red[128 + t] + red[192 + t] + head[L.l1b + t];
-        hv = fmaxf(hsum, 0.0f) * head[L.l2w + t];
-    }
-    __syncthreads();
-    if (writer && (t & 63) == 0) stat[4 + g] = s;
-    if (writer && t < 64) {
-        hv = t_wave_sum(hv);
-        if (t == 0) red[0] = tanhf(hv + head[L.l2b]);
-    }
-    __syncthreads();
-    const float sum = stat[4] + stat[5] + stat[6] + stat[7];
-    const float value = red[0];
-    if (valid) {
+    for (int bb = 0; bb < NB; bb++) {
+        if (b0 + bb >= nb) break;
+        const float* st = stat + bb * (2 * NW + 4);
+        float sum = 0.0f;
+        for (int i = 0; i < NW; i++) sum += st[NW + i];
+        const float value = st[2 * NW];
+        const int row = row0 + b0 + bb;
+        const float* lb = lg + bb * 4096;
         if constexpr (!SEARCH) {
             float* pr = pol_out + (size_t)row * 4096;
-            for (int i = t; i < 4096; i += 256) pr[i] = expf(lg[i] - mx) / sum;
-            if (t == 0) val_out[row] = value;
+            for (int i = tid; i < 4096; i += NT) pr[i] = expf(lb[i] - mx[bb]) / sum;
+            if (tid == 0) val_out[row] = value;
         } else {
             const int game = so.row_game[row], node = so.row_node[row];
             const Node nd = so.nodes[(size_t)game * so.NMAX + node];
             Edge* e = so.edges + (size_t)game * so.EMAX + nd.edge_begin;
-            for (int i = t; i < nd.nedges; i += 256) {
+            const int* sl = reinterpret_cast<const int*>(st + 2 * NW + 1);
+            const int slot = so.log_cap > 0 ? sl[0] : -1;
+            for (int i = tid; i < nd.nedges; i += NT) {
                 const int idx = e[i].idx & azc::IDX_MASK;
-                e[i].P = expf(lg[idx] - mx) / sum;
-            }
-            if (t == 0) so.value[row] = value;
-            if (so.log_cap > 0) {
-                int* slot = reinterpret_cast<int*>(stat + 8);
-                if (t == 0) {
-                    const int r = atomicAdd(&so.ctr->log_count, 1);
-                    const int po = atomicAdd(&so.ctr->log_prior_count, (int)nd.nedges);
-                    slot[0] = (r < so.log_cap && po + nd.nedges <= so.log_prior_cap) ? r : -1;
-                    slot[1] = po;
-                    if (slot[0] >= 0) {
-                        so.log_key[r] = azc::fen_key(so.npos[(size_t)game * so.NMAX + node]);
-                        so.log_value[r] = value;
-                        so.log_off[r] = po;
-                        so.log_n[r] = nd.nedges;
-                    }
+                const float P = expf(lb[idx] - mx[bb]) / sum;
+                e[i].P = P;
+                if (slot >= 0) {
+                    so.log_idx[sl[1] + i] = idx;
+                    so.log_prior[sl[1] + i] = P;
                 }
-                // slot[] (thread 0) is read by the caller after the next __syncthreads
+            }
+            if (tid == 0) {
+                so.value[row] = value;
+                if (slot >= 0) {
+                    so.log_key[slot] = azc::fen_key(so.npos[(size_t)game * so.NMAX + node]);
+                    so.log_value[slot] = value;
+                    so.log_off[slot] = sl[1];
+                    so.log_n[slot] = nd.nedges;
+                }
             }
         }
     }
+    __syncthreads();
 }
 
 template <int F, bool SEARCH>
@@ -311,18 +432,31 @@ tower_kernel(const __bf16* __restrict__ planes, TowerArgs ta, const int* __restr
     constexpr int RSF = F / 8 + 2, RSI = 32 / 8 + 2;
     constexpr int XSZ = BPB * 64 * RSF;               // slots per activation buffer
     constexpr int ZN = 16 + F / 8;
-    constexpr int HEADS_FLOATS = 32 * 64 + 8 * 64 + 4096 + 256 + 16;
-    constexpr int PAR = NT / 256 < BPB ? NT / 256 : BPB;   // boards whose heads run concurrently
-    static_assert(NT % 256 == 0, "heads need 256-thread groups");
-    static_assert(PAR * HEADS_FLOATS * 4 <= XSZ * 16, "heads scratch must fit in h");
     __shared__ __attribute__((aligned(16))) uint4 lds[2 * XSZ + ZN];
     const int count = count_ptr ? min(*count_ptr, rows) : rows;
     const int row0 = blockIdx.x * BPB;
     if (row0 >= count) return;
     const int nb = min(BPB, count - row0);
     const int tid = threadIdx.x, lane = tid & 63;
+    TR_STAMP(0);
+#ifdef AZ_TOWER_TRACE
+    if (tid == 0) ta.trace[(size_t)blockIdx.x * TR_SLOTS + 112] = __builtin_amdgcn_s_memtime();
+    if (lane == 0) {
+        unsigned hww;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hww));
+        ta.trace[(size_t)blockIdx.x * TR_SLOTS + 114 + (tid >> 6)] = hww;
+    }
+    if (tid == 0) {
+        unsigned hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        ta.trace[(size_t)blockIdx.x * TR_SLOTS + 47] = ((unsigned long long)xcc << 32) | hw;
+    }
+#endif
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int cw = w % NCW, bw = w / NCW;
+    const int wpar = (w >> 2) & 1;                    // waves w and w+4 share a SIMD
     uint4* X = lds;
     uint4* H = lds + XSZ;
     const int zero_off = 2 * XSZ * 16;
@@ -336,46 +470,48 @@ tower_kernel(const __bf16* __restrict__ planes, TowerArgs ta, const int* __restr
     }
     for (int c = tid; c < ZN; c += NT) lds[2 * XSZ + c] = make_uint4(0, 0, 0, 0);
     __syncthreads();
+    TR_STAMP(1);
     {
         uint4 wr0[RingPF<1>::PF][NCO];
         ring_fill<1, F, NCO>(wr0, ta.w[0], cw, lane);
         conv_lds<32, RSI, F, RSF, BPW, NCO, false>(ldsb, X, XSZ * 16, zero_off, ta.w[0], nullptr, ta.b[0], wr0, cw,
-                                                   bw, lane);
+                                                   bw, lane, wpar);
     }
+    TR_STAMP(2);
     uint4 wr[RingPF<F / 32>::PF][NCO];
     if (ta.blocks > 0) ring_fill<F / 32, F, NCO>(wr, ta.w[1], cw, lane);
     for (int b = 0; b < ta.blocks; b++) {
         const uint4* after = b + 1 < ta.blocks ? ta.w[3 + 2 * b] : nullptr;
+#ifdef AZ_TOWER_TRACE
+        unsigned long long* trw = b == 10 ? ta.trace + (size_t)blockIdx.x * TR_SLOTS + 48 + w * 8 : nullptr;
+#else
+        unsigned long long* trw = nullptr;
+#endif
         conv_lds<F, RSF, F, RSF, BPW, NCO, false>(ldsb, H, 0, zero_off, ta.w[1 + 2 * b], ta.w[2 + 2 * b],
-                                                  ta.b[1 + 2 * b], wr, cw, bw, lane);
+                                                  ta.b[1 + 2 * b], wr, cw, bw, lane, wpar, trw);
         conv_lds<F, RSF, F, RSF, BPW, NCO, true>(ldsb, X, XSZ * 16, zero_off, ta.w[2 + 2 * b], after, ta.b[2 + 2 * b],
-                                                 wr, cw, bw, lane);
+                                                 wr, cw, bw, lane, wpar, trw ? trw + 4 : nullptr);
+        TR_STAMP(3 + b);
     }
-    // heads: 256-thread groups, PAR boards at a time, scratch in H
-    const int grp = tid >> 8, t = tid & 255;
-    float* scratch = reinterpret_cast<float*>(H) + (grp < PAR ? grp : 0) * HEADS_FLOATS;
-    for (int b0 = 0; b0 < BPB; b0 += PAR) {
-        const int b = b0 + grp;
-        const bool valid = grp < PAR && b < nb;
-        heads_lds<F, RSF, SEARCH>(ldsb + (size_t)(b < BPB ? b : 0) * 64 * RSF * 16, scratch, t, ta.head, grp < PAR,
-                                  valid, row0 + b, pol_out, val_out, so);
-        __syncthreads();
-        if constexpr (SEARCH) {
-            if (valid && so.log_cap > 0) {
-                const int* slot = reinterpret_cast<const int*>(scratch + 32 * 64 + 8 * 64 + 4096 + 256 + 8);
-                if (slot[0] >= 0) {
-                    const int game = so.row_game[row0 + b], node = so.row_node[row0 + b];
-                    const Node nd = so.nodes[(size_t)game * so.NMAX + node];
-                    const Edge* e = so.edges + (size_t)game * so.EMAX + nd.edge_begin;
-                    for (int i = t; i < nd.nedges; i += 256) {
-                        so.log_idx[slot[1] + i] = e[i].idx & azc::IDX_MASK;
-                        so.log_prior[slot[1] + i] = e[i].P;
-                    }
-                }
-            }
-        }
-        __syncthreads();
+    // heads: NB boards at a time, scratch in H
+    {
+        constexpr int NB = HeadsCfg<F>::NB;
+        static_assert(HeadsScratch<NB, NT>::FLOATS * 4 <= XSZ * 16, "heads scratch must fit in h");
+        static_assert((16 * NB) % (NT / 64) == 0, "policy tiles must divide over the waves");
+        for (int b0 = 0; b0 < BPB && b0 < nb; b0 += NB)
+            heads_group<F, RSF, NB, NT, SEARCH>(ldsb, reinterpret_cast<float*>(H), b0, nb, row0, tid, ta.head_frag,
+                                                ta.head, pol_out, val_out, so,
+#ifdef AZ_TOWER_TRACE
+                                                b0 == 0 ? ta.trace + (size_t)blockIdx.x * TR_SLOTS + 122 : nullptr
+#else
+                                                nullptr
+#endif
+            );
     }
+    TR_STAMP(45);
+#ifdef AZ_TOWER_TRACE
+    if (tid == 0) ta.trace[(size_t)blockIdx.x * TR_SLOTS + 113] = __builtin_amdgcn_s_memtime();
+#endif
 }
 
 bool tower_supported(const NetDev* n) {
@@ -390,14 +526,42 @@ int tower_forward(NetDev* n, const void* planes, const int* count, int rows, flo
     TowerArgs ta;
     memset(&ta, 0, sizeof(ta));
     for (int i = 0; i < 1 + 2 * n->blocks; i++) {
-        ta.w[i] = reinterpret_cast<const uint4*>(n->conv_w[i]);
-        ta.b[i] = n->conv_b[i];
+#ifdef AZ_TOWER_SAMEW   // experiment only: every residual conv reads block 0's weights (L2-resident)
+        const int src = i == 0 ? 0 : 1 + ((i - 1) & 1);
+#else
+        const int src = i;
+#endif
+        ta.w[i] = reinterpret_cast<const uint4*>(n->conv_w[src]);
+        ta.b[i] = n->conv_b[src];
     }
     ta.head = n->head;
+    ta.head_frag = reinterpret_cast<const uint4*>(n->head_frag);
     ta.blocks = n->blocks;
+#ifdef AZ_TOWER_TRACE
+    // experiment only: stamp launch number AZ_TOWER_TRACE of this process into $AZ_TOWER_TRACE_FILE
+    static unsigned long long* trbuf = nullptr;
+    static int launch_no = 0;
+    if (!trbuf) (void)hipMalloc(&trbuf, (size_t)(rows + 8) * TR_SLOTS * 8);
+    ta.trace = trbuf;
+    const bool dump = ++launch_no == AZ_TOWER_TRACE;
+#endif
     SearchOut dummy;
     memset(&dummy, 0, sizeof(dummy));
     const SearchOut& s = so ? *so : dummy;
+#ifdef AZ_TOWER_TRACE
+#define TRACE_DUMP(grid)                                                                                   \
+    if (dump) {                                                                                            \
+        std::vector<unsigned long long> h((size_t)(grid) * TR_SLOTS);                                      \
+        (void)hipStreamSynchronize(st);                                                                    \
+        (void)hipMemcpy(h.data(), trbuf, h.size() * 8, hipMemcpyDeviceToHost);                             \
+        if (FILE* f = fopen(getenv("AZ_TOWER_TRACE_FILE") ? getenv("AZ_TOWER_TRACE_FILE") : "tower_trace.bin", "wb")) { \
+            fwrite(h.data(), 8, h.size(), f);                                                              \
+            fclose(f);                                                                                     \
+        }                                                                                                  \
+    }
+#else
+#define TRACE_DUMP(grid)
+#endif
 #define AZ_TOWER(FF)                                                                                           \
     if (n->filters == FF) {                                                                                    \
         constexpr int BPB = TowerCfg<FF>::BPB;                                                                 \
@@ -405,6 +569,7 @@ int tower_forward(NetDev* n, const void* planes, const int* count, int rows, flo
         const int grid = (rows + BPB - 1) / BPB;                                                               \
         if (so) tower_kernel<FF, true><<<grid, NT, 0, st>>>((const __bf16*)planes, ta, count, rows, pol, val, s); \
         else tower_kernel<FF, false><<<grid, NT, 0, st>>>((const __bf16*)planes, ta, count, rows, pol, val, s);  \
+        TRACE_DUMP(grid);                                                                                      \
         return hipGetLastError() == hipSuccess ? 0 : fail("tower launch failed");                              \
     }
     AZ_TOWER(256) AZ_TOWER(128) AZ_TOWER(64) AZ_TOWER(32)
