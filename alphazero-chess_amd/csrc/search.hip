@@ -69,6 +69,10 @@ __global__ void __launch_bounds__(256) k_select(Engine E) {
             if (ob > best || (ob == best && op < bpos)) { best = ob; bpos = op; }
         }
         bytes += 16ull * nd.nedges + 16ull + 4ull;
+        // no edge beat -inf: every value is NaN (a diverged network).  The reference keeps its
+        // initial idx (tree.rs:121-131); the engine takes the first edge instead of reading
+        // past the node's edge list.
+        if (bpos >= nd.nedges) bpos = 0;
         const int eabs = nd.edge_begin + bpos;
         if (lane == 0) { pn[len] = node; pe[len] = eabs; }
         const int child = edges[eabs].child;

@@ -28,6 +28,12 @@
                            // PRIO k-steps: without it the older wave races ahead and the other
                            // finishes its layer alone, latency-bound (0 = off)
 #endif
+#ifndef AZ_TOWER_FLAGS
+#define AZ_TOWER_FLAGS 0   // 1: F = 256 residual convs hand off through per-wave LDS flags (wait_done); measured 7 % slower
+#endif
+#ifndef AZ_TOWER_AACC
+#define AZ_TOWER_AACC 0    // 1: residual-conv MFMAs as inline asm with AGPR accumulators
+#endif
 #ifndef AZ_TOWER_LA
 #define AZ_TOWER_LA 4      // activation (B-fragment) LDS reads issued this many fragments ahead
 #endif
@@ -95,22 +101,48 @@ __device__ __forceinline__ void ring_fill(uint4 (&wr)[RingPF<NCH>::PF][NCO], con
         for (int n = 0; n < NCO; n++) wr[i][n] = W[(size_t)i * CF * 64 + n * 64];
 }
 
+// Layer hand-off without a workgroup barrier (NSPLIT = 2, F = 256): wave w publishes in
+// done[w] the index of the last layer whose epilogue it has written; a wave reads input
+// chunk c (32 channels, written by wave c) of layer L only once done[c] >= L - 1.  The k-steps
+// run chunk group by chunk group (chunks 0-3, all taps; then 4-7), so the older waves 0-3,
+// which win issue arbitration and finish a layer first, start the next one on their own
+// chunks while their younger SIMD partners finish: no wave is left alone on its SIMD
+// (measured: a lone wave keeps the matrix pipe ~40-50 % busy).  No WAR check is needed: a wave
+// reaches its epilogue of layer L+1 only after reading every chunk of layer L, i.e. after every
+// wave has finished layer L.  Bounded spin (a hand-off bug gives wrong results, not a hang).
+__device__ __forceinline__ void wait_done(const int* done, int c0, int n, int need) {
+    for (int c = c0; c < c0 + n; c++)
+        for (int it = 0; *reinterpret_cast<const volatile int*>(done + c) < need && it < (1 << 20); it++)
+            __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+}
+
 // wr: register ring holding this layer's next PF weight k-steps on entry; on exit it holds
 // the first PF k-steps of `wnext` (the next layer with the same chunk count), or zeros.
-template <int CIN, int RSI, int F, int RSO, int BPW, int NCO, bool RESID>
+template <int CIN, int RSI, int F, int RSO, int BPW, int NCO, bool RESID, int NSPLIT = 1>
 __device__ __forceinline__ void conv_lds(const char* __restrict__ ldsb, uint4* __restrict__ out_lds, int in_off,
                                          int zero_off, const uint4* __restrict__ wsw, const uint4* __restrict__ wnext,
                                          const float* __restrict__ bias, uint4 (&wr)[RingPF<CIN / 32>::PF][NCO],
-                                         int cw, int bw, int lane, int wpar, unsigned long long* trw = nullptr) {
+                                         int cw, int bw, int lane, int wpar, unsigned long long* trw = nullptr,
+                                         int* done = nullptr, int lidx = 0) {
     constexpr int NCH = CIN / 32;                     // 32-channel K chunks (4 slots)
     if (trw && lane == 0) trw[0] = __builtin_amdgcn_s_memtime();
+#ifdef AZ_TOWER_SOLO   // experiment only: waves 4-7 skip the residual convs (waves 0-3 run alone on their SIMDs)
+    if (CIN > 32 && cw >= 4) {
+        if (trw && lane == 0) trw[1] = trw[2] = __builtin_amdgcn_s_memtime();
+        __syncthreads();
+        if (trw && lane == 0) trw[3] = __builtin_amdgcn_s_memtime();
+        return;
+    }
+#endif
     constexpr int CF = F / 16;
     constexpr int MF = BPW * 4;
     constexpr int KS = 9 * NCH;
+    constexpr int CPH = NCH / NSPLIT;                 // chunks per group
     // weight fragments are prefetched PF k-steps ahead through a register ring; PF divides
-    // NCH so the ring slot of every k-step is a compile-time constant
+    // the group's chunk count so the ring slot of every k-step is a compile-time constant
     constexpr int PF = RingPF<NCH>::PF;
-    static_assert(NCH % PF == 0, "prefetch depth must divide the chunk count");
+    static_assert(NCH % NSPLIT == 0 && CPH % PF == 0, "prefetch depth must divide the chunk group");
     const int h = lane >> 4;
     // accumulators start at the folded bias: no bias adds in the epilogue
     f32x4 acc[MF][NCO];
@@ -122,77 +154,111 @@ __device__ __forceinline__ void conv_lds(const char* __restrict__ ldsb, uint4* _
     }
     const uint4* W = wsw + (size_t)(cw * NCO) * 64 + lane;
     // past the last k-step the refills read the next layer (or this layer's zero padding)
-    const uint4* Wn = (wnext ? wnext + (size_t)(cw * NCO) * 64 + lane : W + (size_t)KS * CF * 64) - (size_t)KS * CF * 64;
+    const uint4* Wn = wnext ? wnext + (size_t)(cw * NCO) * 64 + lane : W + (size_t)KS * CF * 64;
     // B-fragment (activation) reads run LA fragments ahead, across k-step and tap boundaries:
-    // the first LA reads of step s+1 are issued inside step s.
+    // the first LA reads of step s+1 are issued inside step s (not across a chunk-group
+    // boundary, where the producers' flags are checked first).
     constexpr int LA = AZ_TOWER_LA < MF ? AZ_TOWER_LA : MF;
     static_assert(MF % LA == 0, "read-ahead ring must tile the fragment loop");
+    // Per-tap LDS addresses of the B fragments, branch-free (the tap loop is not unrolled, so
+    // each tap boundary runs this once; a branchy form cost ~150 instructions per tap, which
+    // a wave alone on its SIMD pays as matrix-pipe idle time).  Valid taps read the shifted
+    // square; off-board taps read the zero row at the same 16-B slot mod 16 (conflict-free):
+    // in_off and zero_off are multiples of 256 B and every row offset keeps the slot, so the
+    // zero address is zero_off | (valid-form address & 0xF0).
+    const int lane_off = (((lane & 15) * RSI) + h) * 16;
+    const int lr = (lane & 15) >> 3, lf = lane & 7;
     auto tap_bases = [&](int tap, int* base) {
         const int dr = tap / 3 - 1, df = tap % 3 - 1;
+        const bool okf = (unsigned)(lf + df) < 8u;
 #pragma unroll
-        for (int m = 0; m < MF; m++) {
-            const int b = bw * BPW + (m >> 2);
-            const int sq = (m & 3) * 16 + (lane & 15);
-            const int r = (sq >> 3) + dr, f = (sq & 7) + df;
-            const bool ok = (unsigned)r < 8u && (unsigned)f < 8u;
-            const int s2 = (r * 8 + f) & 63;
-            base[m] = ok ? in_off + ((b * 64 + s2) * RSI + h) * 16 : zero_off + (((s2 * RSI) & 15) + h) * 16;
+        for (int q = 0; q < 4; q++) {
+            const bool ok = okf && (unsigned)(2 * q + lr + dr) < 8u;
+#pragma unroll
+            for (int bb = 0; bb < BPW; bb++) {
+                const int m = bb * 4 + q;
+                const int va = lane_off + (((bw * BPW + bb) * 64 + q * 16 + dr * 8 + df) * RSI) * 16 + in_off;
+                const int vz = (va & 0xF0) | zero_off;
+                base[m] = ok ? va : vz;
+            }
         }
     };
     int bcur[MF], bnext[MF];
-    tap_bases(0, bcur);
     uint4 bq[LA];
 #pragma unroll
-    for (int m = 0; m < LA; m++) bq[m] = *reinterpret_cast<const uint4*>(ldsb + bcur[m]);
-    for (int tap = 0; tap < 9; tap++) {
-        tap_bases(tap < 8 ? tap + 1 : 8, bnext);
+    for (int half = 0; half < NSPLIT; half++) {
+        if constexpr (NSPLIT > 1) wait_done(done, half * CPH, CPH, lidx - 1);
+        tap_bases(0, bcur);
 #pragma unroll
-        for (int cc = 0; cc < NCH; cc++) {
-            const int ks = tap * NCH + cc;
-            if constexpr (AZ_TOWER_PRIO > 0) {
-                if ((((cc / AZ_TOWER_PRIO) & 1) ^ wpar) != 0) __builtin_amdgcn_s_setprio(1);
-                else __builtin_amdgcn_s_setprio(0);
-            }
-            uint4 a[NCO];
+        for (int m = 0; m < LA; m++) bq[m] = *reinterpret_cast<const uint4*>(ldsb + bcur[m] + half * CPH * 64);
+        for (int tap = 0; tap < 9; tap++) {
+            tap_bases(tap < 8 ? tap + 1 : 8, bnext);
 #pragma unroll
-            for (int n = 0; n < NCO; n++) a[n] = wr[cc % PF][n];
-            // refill this ring slot with k-step ks+PF (of the next layer once past the end)
-            const uint4* Wsrc = (tap == 8 && cc + PF >= NCH) ? Wn : W;
-#pragma unroll
-#ifdef AZ_TOWER_L1W   // experiment only: every k-step re-reads k-steps 0..1 (L1-resident weights)
-            for (int n = 0; n < NCO; n++) wr[cc % PF][n] = W[(size_t)((ks + PF) & 1) * CF * 64 + n * 64];
-            (void)Wsrc;
-#else
-            for (int n = 0; n < NCO; n++) wr[cc % PF][n] = Wsrc[(size_t)(ks + PF) * CF * 64 + n * 64];
-#endif
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int m = 0; m < MF; m++) {
-                const uint4 bv = bq[m % LA];
-                if (m + LA < MF) {
-                    bq[m % LA] = *reinterpret_cast<const uint4*>(ldsb + bcur[m + LA] + cc * 64);
-                } else if (cc + 1 < NCH) {                   // next k-step, same tap
-                    bq[m % LA] = *reinterpret_cast<const uint4*>(ldsb + bcur[m + LA - MF] + (cc + 1) * 64);
-                } else {                                     // first k-step of the next tap
-                    bq[m % LA] = *reinterpret_cast<const uint4*>(ldsb + bnext[m + LA - MF]);
+            for (int c4 = 0; c4 < CPH; c4++) {
+                const int cc = half * CPH + c4;
+                if constexpr (AZ_TOWER_PRIO > 0) {
+                    if ((((cc / AZ_TOWER_PRIO) & 1) ^ wpar) != 0) __builtin_amdgcn_s_setprio(1);
+                    else __builtin_amdgcn_s_setprio(0);
                 }
-                const bf16x8 Bv = __builtin_bit_cast(bf16x8, bv);
+                uint4 a[NCO];
 #pragma unroll
-                for (int n = 0; n < NCO; n++)
-                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[n]), Bv,
-                                                                        acc[m][n], 0, 0, 0);
+                for (int n = 0; n < NCO; n++) a[n] = wr[c4 % PF][n];
+                // refill this ring slot with the k-step PF positions later in the sequence
+                // (the next tap, the next chunk group, or the next layer once past the end)
+                const uint4* Wsrc;
+                if (c4 + PF < CPH) Wsrc = W + (size_t)(tap * NCH + cc + PF) * CF * 64;
+                else if (tap < 8) Wsrc = W + (size_t)((tap + 1) * NCH + half * CPH + c4 + PF - CPH) * CF * 64;
+                else if (half + 1 < NSPLIT) Wsrc = W + (size_t)((half + 1) * CPH + c4 + PF - CPH) * CF * 64;
+                else Wsrc = Wn + (size_t)(c4 + PF - CPH) * CF * 64;
+#pragma unroll
+#if defined(AZ_TOWER_L1W)   // experiment only: every k-step re-reads k-steps 0..1 (L1-resident weights)
+                for (int n = 0; n < NCO; n++) wr[c4 % PF][n] = W[(size_t)((c4 + PF) & 1) * CF * 64 + n * 64];
+                (void)Wsrc;
+#else
+                for (int n = 0; n < NCO; n++) wr[c4 % PF][n] = Wsrc[n * 64];
+#endif
+                __builtin_amdgcn_sched_barrier(0);
+                const bool last_of_group = tap == 8 && c4 + 1 == CPH && half + 1 < NSPLIT;
+#pragma unroll
+                for (int m = 0; m < MF; m++) {
+                    const uint4 bv = bq[m % LA];
+                    if (m + LA < MF) {
+                        bq[m % LA] = *reinterpret_cast<const uint4*>(ldsb + bcur[m + LA] + cc * 64);
+                    } else if (c4 + 1 < CPH) {                   // next k-step, same tap
+                        bq[m % LA] = *reinterpret_cast<const uint4*>(ldsb + bcur[m + LA - MF] + (cc + 1) * 64);
+                    } else if (!last_of_group) {                 // first k-step of the next tap
+                        bq[m % LA] = *reinterpret_cast<const uint4*>(ldsb + bnext[m + LA - MF] + half * CPH * 64);
+                    }
+                    const bf16x8 Bv = __builtin_bit_cast(bf16x8, bv);
+#pragma unroll
+                    for (int n = 0; n < NCO; n++) {
+#if AZ_TOWER_AACC
+                        // accumulators pinned to AGPRs: no VGPR renaming of C/D through the B registers
+                        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
+                                     : "+a"(acc[m][n])
+                                     : "v"(__builtin_bit_cast(bf16x8, a[n])), "v"(Bv));
+#else
+                        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[n]), Bv,
+                                                                            acc[m][n], 0, 0, 0);
+#endif
+                    }
+                }
+#pragma unroll
+                for (int m = 0; m < MF; m++) {
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, NCO, 0);
+                }
+                __builtin_amdgcn_sched_barrier(0);
             }
 #pragma unroll
-            for (int m = 0; m < MF; m++) {
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, NCO, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
+            for (int m = 0; m < MF; m++) bcur[m] = bnext[m];
         }
-#pragma unroll
-        for (int m = 0; m < MF; m++) bcur[m] = bnext[m];
     }
     (void)KS;
+#if AZ_TOWER_AACC
+    // the compiler does not see the asm MFMAs: cover the XDL-write -> VALU-read hazard by hand
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+#endif
     if constexpr (AZ_TOWER_PRIO > 0) __builtin_amdgcn_s_setprio(0);
     if (trw && lane == 0) trw[1] = __builtin_amdgcn_s_memtime();
     // `in` and `out` are different buffers, so the epilogue needs no barrier before it;
@@ -225,7 +291,13 @@ __device__ __forceinline__ void conv_lds(const char* __restrict__ ldsb, uint4* _
         }
     }
     if (trw && lane == 0) trw[2] = __builtin_amdgcn_s_memtime();
-    __syncthreads();
+    if constexpr (NSPLIT > 1) {
+        // publish: this wave's LDS writes complete, then done[cw] = lidx
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) *reinterpret_cast<volatile int*>(done + cw) = lidx;
+    } else {
+        __syncthreads();
+    }
     if (trw && lane == 0) trw[3] = __builtin_amdgcn_s_memtime();
 }
 
@@ -432,7 +504,9 @@ tower_kernel(const __bf16* __restrict__ planes, TowerArgs ta, const int* __restr
     constexpr int RSF = F / 8 + 2, RSI = 32 / 8 + 2;
     constexpr int XSZ = BPB * 64 * RSF;               // slots per activation buffer
     constexpr int ZN = 16 + F / 8;
-    __shared__ __attribute__((aligned(16))) uint4 lds[2 * XSZ + ZN];
+    // chunk-group split + per-wave done flags (no barrier between residual convs): F = 256 only
+    constexpr int NSP = (AZ_TOWER_FLAGS && F == 256 && WB == 1) ? 2 : 1;
+    __shared__ __attribute__((aligned(16))) uint4 lds[2 * XSZ + ZN + 2];
     const int count = count_ptr ? min(*count_ptr, rows) : rows;
     const int row0 = blockIdx.x * BPB;
     if (row0 >= count) return;
@@ -457,6 +531,9 @@ tower_kernel(const __bf16* __restrict__ planes, TowerArgs ta, const int* __restr
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int cw = w % NCW, bw = w / NCW;
     const int wpar = (w >> 2) & 1;                    // waves w and w+4 share a SIMD
+#ifdef AZ_TOWER_YPRIO   // experiment: static priority for the younger half (guide T5 static form)
+    if (w >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
     uint4* X = lds;
     uint4* H = lds + XSZ;
     const int zero_off = 2 * XSZ * 16;
@@ -469,6 +546,8 @@ tower_kernel(const __bf16* __restrict__ planes, TowerArgs ta, const int* __restr
         H[rowi * RSI + slot] = rowi < nb * 64 ? src[c] : make_uint4(0, 0, 0, 0);
     }
     for (int c = tid; c < ZN; c += NT) lds[2 * XSZ + c] = make_uint4(0, 0, 0, 0);
+    int* done = reinterpret_cast<int*>(lds + 2 * XSZ + ZN);   // [8] last layer whose epilogue wave w wrote
+    if (tid < 8) done[tid] = 0;                              // layer 0 = the input conv (barrier after it)
     __syncthreads();
     TR_STAMP(1);
     {
@@ -487,12 +566,14 @@ tower_kernel(const __bf16* __restrict__ planes, TowerArgs ta, const int* __restr
 #else
         unsigned long long* trw = nullptr;
 #endif
-        conv_lds<F, RSF, F, RSF, BPW, NCO, false>(ldsb, H, 0, zero_off, ta.w[1 + 2 * b], ta.w[2 + 2 * b],
-                                                  ta.b[1 + 2 * b], wr, cw, bw, lane, wpar, trw);
-        conv_lds<F, RSF, F, RSF, BPW, NCO, true>(ldsb, X, XSZ * 16, zero_off, ta.w[2 + 2 * b], after, ta.b[2 + 2 * b],
-                                                 wr, cw, bw, lane, wpar, trw ? trw + 4 : nullptr);
+        conv_lds<F, RSF, F, RSF, BPW, NCO, false, NSP>(ldsb, H, 0, zero_off, ta.w[1 + 2 * b], ta.w[2 + 2 * b],
+                                                       ta.b[1 + 2 * b], wr, cw, bw, lane, wpar, trw, done, 1 + 2 * b);
+        conv_lds<F, RSF, F, RSF, BPW, NCO, true, NSP>(ldsb, X, XSZ * 16, zero_off, ta.w[2 + 2 * b], after,
+                                                      ta.b[2 + 2 * b], wr, cw, bw, lane, wpar,
+                                                      trw ? trw + 4 : nullptr, done, 2 + 2 * b);
         TR_STAMP(3 + b);
     }
+    if constexpr (NSP > 1) __syncthreads();           // the heads read every channel
     // heads: NB boards at a time, scratch in H
     {
         constexpr int NB = HeadsCfg<F>::NB;

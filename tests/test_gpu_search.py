@@ -154,3 +154,17 @@ def test_fen_cache_search_bit_exact(require_gpu):
     for g, h in enumerate(hs):
         rv, ri, rd, _ = O.search_game(cfg, h, noise=True, noise_key=O.lib().ref_stream_key(4, g, len(h), 0))
         assert np.array_equal(vis[g].astype(np.float32), rv) and dep[g] == rd
+
+
+def test_search_survives_nan_network(require_gpu):
+    """A diverged network (NaN everywhere) must not take the engine out of bounds: every PUCT
+    value is NaN, nothing beats -inf, and the walk takes the first edge (the reference keeps
+    its initial index, tree.rs:121-131).  The search completes with every simulation counted."""
+    w = A.random_weights(2, 32, seed=5)
+    w[:] = np.nan
+    net = A.AlphaZero(2, 32, weights=w, dtype="bf16")
+    s = A.BatchedSearch(net, games=4, sims=64, seed=1)
+    s.set_roots([[], [588], [], [588]], apply_noise=True)
+    imp, vis, dep = s.run()
+    assert np.all(vis.sum(axis=1) == 64)
+    assert np.all((dep >= 1) & (dep <= 64))
