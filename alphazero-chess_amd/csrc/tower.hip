@@ -72,7 +72,7 @@ constexpr int TR_SLOTS = 128;
 template <int F> struct TowerCfg;
 template <> struct TowerCfg<256> { static constexpr int BPB = 2, WB = AZ_TOWER_WB256, NCO = AZ_TOWER_NCO256; };
 template <> struct TowerCfg<128> { static constexpr int BPB = 4, WB = 1, NCO = 2; };
-template <> struct TowerCfg<64> { static constexpr int BPB = 4, WB = 2, NCO = 2; };
+template <> struct TowerCfg<64> { static constexpr int BPB = 1, WB = 1, NCO = 2; };   // C2: 256 games -> 256 workgroups
 template <> struct TowerCfg<32> { static constexpr int BPB = 8, WB = 4, NCO = 2; };
 
 __device__ __forceinline__ float t_wave_max(float v) {
@@ -222,6 +222,7 @@ __device__ __forceinline__ void conv_lds(const char* __restrict__ ldsb, uint4* _
 #pragma unroll
                 for (int m = 0; m < MF; m++) {
                     const uint4 bv = bq[m % LA];
+#ifndef AZ_TOWER_NOLDSR   // (experiment only: no activation reads inside the loop)
                     if (m + LA < MF) {
                         bq[m % LA] = *reinterpret_cast<const uint4*>(ldsb + bcur[m + LA] + cc * 64);
                     } else if (c4 + 1 < CPH) {                   // next k-step, same tap
@@ -229,6 +230,7 @@ __device__ __forceinline__ void conv_lds(const char* __restrict__ ldsb, uint4* _
                     } else if (!last_of_group) {                 // first k-step of the next tap
                         bq[m % LA] = *reinterpret_cast<const uint4*>(ldsb + bnext[m + LA - MF] + half * CPH * 64);
                     }
+#endif
                     const bf16x8 Bv = __builtin_bit_cast(bf16x8, bv);
 #pragma unroll
                     for (int n = 0; n < NCO; n++) {
@@ -504,9 +506,12 @@ tower_kernel(const __bf16* __restrict__ planes, TowerArgs ta, const int* __restr
     constexpr int RSF = F / 8 + 2, RSI = 32 / 8 + 2;
     constexpr int XSZ = BPB * 64 * RSF;               // slots per activation buffer
     constexpr int ZN = 16 + F / 8;
+    // h doubles as the heads' scratch: at least that large (small nets with 1 board per workgroup)
+    constexpr int HSZ0 = (HeadsScratch<HeadsCfg<F>::NB, NT>::FLOATS * 4 + 15) / 16;
+    constexpr int HSZ = ((XSZ > HSZ0 ? XSZ : HSZ0) + 15) / 16 * 16;
     // chunk-group split + per-wave done flags (no barrier between residual convs): F = 256 only
     constexpr int NSP = (AZ_TOWER_FLAGS && F == 256 && WB == 1) ? 2 : 1;
-    __shared__ __attribute__((aligned(16))) uint4 lds[2 * XSZ + ZN + 2];
+    __shared__ __attribute__((aligned(16))) uint4 lds[XSZ + HSZ + ZN + 2];
     const int count = count_ptr ? min(*count_ptr, rows) : rows;
     const int row0 = blockIdx.x * BPB;
     if (row0 >= count) return;
@@ -536,7 +541,7 @@ tower_kernel(const __bf16* __restrict__ planes, TowerArgs ta, const int* __restr
 #endif
     uint4* X = lds;
     uint4* H = lds + XSZ;
-    const int zero_off = 2 * XSZ * 16;
+    const int zero_off = (XSZ + HSZ) * 16;
     const char* ldsb = reinterpret_cast<const char*>(lds);
 
     // stage the input planes [row][64][32] into H with row stride RSI
@@ -545,8 +550,8 @@ tower_kernel(const __bf16* __restrict__ planes, TowerArgs ta, const int* __restr
         const int rowi = c >> 2, slot = c & 3;
         H[rowi * RSI + slot] = rowi < nb * 64 ? src[c] : make_uint4(0, 0, 0, 0);
     }
-    for (int c = tid; c < ZN; c += NT) lds[2 * XSZ + c] = make_uint4(0, 0, 0, 0);
-    int* done = reinterpret_cast<int*>(lds + 2 * XSZ + ZN);   // [8] last layer whose epilogue wave w wrote
+    for (int c = tid; c < ZN; c += NT) lds[XSZ + HSZ + c] = make_uint4(0, 0, 0, 0);
+    int* done = reinterpret_cast<int*>(lds + XSZ + HSZ + ZN);   // [8] last layer whose epilogue wave w wrote
     if (tid < 8) done[tid] = 0;                              // layer 0 = the input conv (barrier after it)
     __syncthreads();
     TR_STAMP(1);
@@ -577,7 +582,7 @@ tower_kernel(const __bf16* __restrict__ planes, TowerArgs ta, const int* __restr
     // heads: NB boards at a time, scratch in H
     {
         constexpr int NB = HeadsCfg<F>::NB;
-        static_assert(HeadsScratch<NB, NT>::FLOATS * 4 <= XSZ * 16, "heads scratch must fit in h");
+        static_assert(HeadsScratch<NB, NT>::FLOATS * 4 <= HSZ * 16, "heads scratch must fit in h");
         static_assert((16 * NB) % (NT / 64) == 0, "policy tiles must divide over the waves");
         for (int b0 = 0; b0 < BPB && b0 < nb; b0 += NB)
             heads_group<F, RSF, NB, NT, SEARCH>(ldsb, reinterpret_cast<float*>(H), b0, nb, row0, tid, ta.head_frag,
@@ -607,11 +612,7 @@ int tower_forward(NetDev* n, const void* planes, const int* count, int rows, flo
     TowerArgs ta;
     memset(&ta, 0, sizeof(ta));
     for (int i = 0; i < 1 + 2 * n->blocks; i++) {
-#ifdef AZ_TOWER_SAMEW   // experiment only: every residual conv reads block 0's weights (L2-resident)
-        const int src = i == 0 ? 0 : 1 + ((i - 1) & 1);
-#else
         const int src = i;
-#endif
         ta.w[i] = reinterpret_cast<const uint4*>(n->conv_w[src]);
         ta.b[i] = n->conv_b[src];
     }
