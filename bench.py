@@ -154,6 +154,15 @@ def net_flop_per_eval(B, F):
     return 2.0 * 64.0 * (171.0 * F + 18.0 * B * F * F + 40.0 * F + 2048.0) + 2.0 * (32768.0 + 64.0)
 
 
+def config_name(games, sims, blocks, filters):
+    """Which BASELINE.json config this run is: C3 = configs[2] (the headline), C2 = configs[1]."""
+    if (sims, blocks, filters) == (800, 20, 256) and games == 2048:
+        return "C3 (BASELINE.json configs[2])"
+    if (sims, blocks, filters) == (800, 6, 64) and games == 256:
+        return "C2 (BASELINE.json configs[1])"
+    return "custom (not a BASELINE.json config)"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -272,8 +281,8 @@ def main():
         "dtype": args.dtype,
         "data": "synthetic: random-init %dx%d weights (seed 42), self-play from startpos, Dirichlet noise on"
                 % (args.blocks, args.filters),
-        "config": {"workload": "C3 (BASELINE.json configs[2]): %d concurrent self-play games/GPU x %d sims/move, "
-                               "%d-block x %d-filter net" % (G, S, args.blocks, args.filters),
+        "config": {"workload": "%s: %d concurrent self-play games/GPU x %d sims/move, %d-block x %d-filter net"
+                               % (config_name(G, S, args.blocks, args.filters), G, S, args.blocks, args.filters),
                    "games_per_gpu": G, "sims_per_move": S, "blocks": args.blocks, "filters": args.filters,
                    "fen_cache": "off for value (see with_fen_cache)",
                    "parallelism": "games sharded %d-way, no collective (gloo barrier/max only)" % world},
