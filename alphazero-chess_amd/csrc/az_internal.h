@@ -97,6 +97,8 @@ struct Engine {
     int* c_n;
     float* c_pri;                          // [slots][MAX_EDGES]
     float* cached_value;                   // [G] value of a cache-served leaf
+    unsigned long long* g_sims;            // [G] simulations backed up (summed at readout)
+    unsigned long long* g_sel_bytes;       // [G] algorithmic bytes read by k_select
     // evaluation log
     int log_cap, log_prior_cap;
     unsigned long long* log_key; float* log_value; int* log_off; int* log_n; int* log_idx; float* log_prior;

@@ -41,6 +41,9 @@ __device__ __forceinline__ azc::Pos* game_npos(const Engine& E, int g) { return 
 __global__ void __launch_bounds__(256) k_select(Engine E) {
     const int g = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const int lane = threadIdx.x & 63;
+    // the step's row counter restarts here (k_expand, the next kernel, allocates rows from it;
+    // the previous step's readers all ran before this launch): no memset launch per step
+    if (blockIdx.x == 0 && threadIdx.x == 0) E.ctr->batch_count = 0;
     if (g >= E.G || !E.active[g]) return;
     const Node* nodes = game_nodes(E, g);
     const Edge* edges = game_edges(E, g);
@@ -83,7 +86,7 @@ __global__ void __launch_bounds__(256) k_select(Engine E) {
             E.leaf_edge[g] = eabs;
             E.leaf_len[g] = len;
             E.leaf_kind[g] = child == CHILD_DRAW ? LEAF_DRAW : (child == CHILD_WIN ? LEAF_WIN : LEAF_EVAL);
-            atomicAdd(&E.ctr->select_bytes, bytes);
+            E.g_sel_bytes[g] += bytes;   // per-game slot: no same-address atomic across 2048 waves
         }
         return;
     }
@@ -140,9 +143,12 @@ struct EdgeSink {
     }
 };
 
-__global__ void __launch_bounds__(64) k_expand(Engine E) {
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= E.G || !E.active[g] || E.leaf_kind[g] != LEAF_EVAL) return;
+enum { X_NONE = 0, X_ROW, X_TERMINAL, X_CACHED };
+
+// one game's expansion; returns what the leaf became (X_ROW: new node that needs a network
+// row, *nid_out = its id)
+__device__ __forceinline__ int expand_leaf(const Engine& E, int g, int* nid_out) {
+    if (g >= E.G || !E.active[g] || E.leaf_kind[g] != LEAF_EVAL) return X_NONE;
     Node* nodes = game_nodes(E, g);
     Edge* edges = game_edges(E, g);
     azc::Pos* npos = game_npos(E, g);
@@ -173,14 +179,13 @@ __global__ void __launch_bounds__(64) k_expand(Engine E) {
     if (res != azc::ONGOING) {
         edges[eabs].child = res == azc::DRAW ? CHILD_DRAW : CHILD_WIN;
         E.leaf_kind[g] = res == azc::DRAW ? LEAF_DRAW : LEAF_WIN;
-        atomicAdd(&E.ctr->terminal, 1ull);
-        return;
+        return X_TERMINAL;
     }
     const int nid = E.node_count[g];
     if (nid >= E.NMAX || ebeg + n > E.EMAX) {                // cannot happen with NMAX = S + 2
         E.leaf_kind[g] = LEAF_DRAW;
         atomicAdd(&E.ctr->overflow, 1);
-        return;
+        return X_NONE;
     }
     Node nn;
     nn.edge_begin = (uint32_t)ebeg;
@@ -203,14 +208,40 @@ __global__ void __launch_bounds__(64) k_expand(Engine E) {
             for (int e = 0; e < n; e++) edges[ebeg + e].P = pri[e];
             E.cached_value[g] = E.c_value[sl];
             E.leaf_kind[g] = LEAF_CACHED;
-            atomicAdd(&E.ctr->cache_hits, 1ull);
-            return;
+            return X_CACHED;
         }
     }
-    const int row = atomicAdd(&E.ctr->batch_count, 1);
-    E.row_game[row] = g;
-    E.row_node[row] = nid;
-    E.leaf_row[g] = row;
+    *nid_out = nid;
+    return X_ROW;
+}
+
+// AZ_EXPAND_GPW games per wavefront (lanes >= GPW idle): the per-lane expansion is serial,
+// branchy integer code, so fewer games per wave means less divergence and more CUs in use.
+// Row allocation and the counters are one atomic per wave (ballot + popcount), not per game.
+#ifndef AZ_EXPAND_GPW
+#define AZ_EXPAND_GPW 16
+#endif
+__global__ void __launch_bounds__(64) k_expand(Engine E) {
+    const int lane = threadIdx.x;
+    const int g = lane < AZ_EXPAND_GPW ? blockIdx.x * AZ_EXPAND_GPW + lane : E.G;
+    int nid = -1;
+    const int kind = expand_leaf(E, g, &nid);
+    const unsigned long long mrow = __ballot(kind == X_ROW);
+    if (mrow) {
+        const int leader = __builtin_ctzll(mrow);
+        int base = 0;
+        if (lane == leader) base = atomicAdd(&E.ctr->batch_count, __popcll(mrow));
+        base = __shfl(base, leader, 64);
+        if (kind == X_ROW) {
+            const int row = base + __popcll(mrow & ((1ull << lane) - 1ull));
+            E.row_game[row] = g;
+            E.row_node[row] = nid;
+            E.leaf_row[g] = row;
+        }
+    }
+    const unsigned long long mt = __ballot(kind == X_TERMINAL), mc = __ballot(kind == X_CACHED);
+    if (lane == 0 && mt) atomicAdd(&E.ctr->terminal, (unsigned long long)__popcll(mt));
+    if (lane == 0 && mc) atomicAdd(&E.ctr->cache_hits, (unsigned long long)__popcll(mc));
 }
 
 // ------------------------------------------------------------------ backup
@@ -236,7 +267,7 @@ __global__ void __launch_bounds__(256) k_backup(Engine E, int step) {
         ed->N = (uint16_t)(ed->N + 1);
         nodes[pn[k]].nsum += 1;
     }
-    if (lane == 0) atomicAdd(&E.ctr->sims, 1ull);
+    if (lane == 0) E.g_sims[g] += 1ull;                         // per-game slot, summed at readout
 }
 
 // ------------------------------------------------------------------ roots
@@ -544,28 +575,39 @@ template <typename T> int dalloc(az_search* s, T** p, size_t count) {
 }
 
 constexpr int EV_PER_STEP = 9;
+constexpr int TIMING_EVERY = 8;   // sampled simulation steps in timing mode (az_timing)
+
+// sum of a per-game device counter (infrequent readouts; the stream is synchronised by the caller)
+unsigned long long sum_games(az_search* s, const unsigned long long* d) {
+    std::vector<unsigned long long> h(s->E.G);
+    if (hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+    unsigned long long t = 0;
+    for (unsigned long long v : h) t += v;
+    return t;
+}
 
 int sim_step(az_search* s, int step, hipEvent_t* ev) {
     Engine& E = s->E;
     hipStream_t st = s->st;
     const int G = E.G;
     if (ev) (void)hipEventRecord(ev[0], st);
-    AZ_HIP(hipMemsetAsync(&E.ctr->batch_count, 0, sizeof(int), st));
     k_select<<<(G * 64 + 255) / 256, 256, 0, st>>>(E);
     if (ev) (void)hipEventRecord(ev[1], st);
-    k_expand<<<(G + 63) / 64, 64, 0, st>>>(E);
+    k_expand<<<(G + AZ_EXPAND_GPW - 1) / AZ_EXPAND_GPW, 64, 0, st>>>(E);
     if (ev) (void)hipEventRecord(ev[2], st);
     const int* cnt = &E.ctr->batch_count;
     int rc = 0;
     if (s->cfg.evaluator == AZ_EVAL_NET) {
         NetDev* n = s->net->dev;
-        rc = net_encode_rows(n, E.npos, E.NMAX, E.row_game, E.row_node, cnt, G, s->planes, st);
+        const bool fused = n->fused && tower_supported(n);
+        // the fused tower encodes its rows itself (planes = nullptr): no encode launch
+        if (!fused) rc = net_encode_rows(n, E.npos, E.NMAX, E.row_game, E.row_node, cnt, G, s->planes, st);
         if (rc) return rc;
         if (ev) (void)hipEventRecord(ev[3], st);
-        if (n->fused && tower_supported(n)) {
-            // one launch: 41 convs + heads, activations resident in LDS
+        if (fused) {
+            // one launch: to_tensor + 41 convs + heads, activations resident in LDS
             if (ev) (void)hipEventRecord(ev[7], st);
-            rc = tower_forward(n, s->planes, cnt, G, nullptr, nullptr, &s->so, st);
+            rc = tower_forward(n, nullptr, cnt, G, nullptr, nullptr, &s->so, st);
             if (rc) return rc;
             if (ev) { (void)hipEventRecord(ev[8], st); (void)hipEventRecord(ev[4], st); }
         } else {
@@ -594,11 +636,8 @@ int eval_rows(az_search* s) {
     const int* cnt = &E.ctr->batch_count;
     if (s->cfg.evaluator == AZ_EVAL_NET) {
         NetDev* n = s->net->dev;
+        if (n->fused && tower_supported(n)) return tower_forward(n, nullptr, cnt, E.G, nullptr, nullptr, &s->so, s->st);
         int rc = net_encode_rows(n, E.npos, E.NMAX, E.row_game, E.row_node, cnt, E.G, s->planes, s->st);
-        if (n->fused && tower_supported(n)) {
-            if (!rc) rc = tower_forward(n, s->planes, cnt, E.G, nullptr, nullptr, &s->so, s->st);
-            return rc;
-        }
         if (!rc) rc = net_tower(n, s->planes, cnt, E.G, s->x, s->h, s->st, nullptr, nullptr);
         if (!rc) rc = net_heads_search(n, s->x, cnt, E.G, s->so, s->st);
         return rc;
@@ -616,8 +655,10 @@ int run_sims(az_search* s) {
             s->ev.push_back(e);
         }
     }
+    // timing mode brackets every TIMING_EVERY-th simulation step with events (an event record
+    // costs a few us of GPU time: on every step it was ~20 % of a 6x64 simulation step)
     for (int i = 0; i < S; i++) {
-        int rc = sim_step(s, i, tm ? &s->ev[EV_PER_STEP * i] : nullptr);
+        int rc = sim_step(s, i, tm && i % TIMING_EVERY == 0 ? &s->ev[EV_PER_STEP * i] : nullptr);
         if (rc) return rc;
     }
     if (tm) {
@@ -629,7 +670,7 @@ int run_sims(az_search* s) {
         const double per_row_conv = 2.0 * 64.0 * 9.0 * F * F;
         const double per_row_tower = net ? net_tower_flop_per_eval(s->net->dev->blocks, s->net->dev->filters) : 0.0;
         const bool fused = net && s->net->dev->fused && tower_supported(s->net->dev);
-        for (int i = 0; i < S; i++) {
+        for (int i = 0; i < S; i += TIMING_EVERY) {
             hipEvent_t* e = &s->ev[EV_PER_STEP * i];
             float t[6], tc = 0.0f;
             for (int k = 0; k < 6; k++) (void)hipEventElapsedTime(&t[k], e[k], e[k + 1]);
@@ -802,6 +843,7 @@ int az_search_create(az_net* net, const az_search_cfg* cfg, int device, az_searc
     rc |= dalloc(s, &E.ctr, 1);
     rc |= dalloc(s, &E.batch_hist, S);
     rc |= dalloc(s, &E.cached_value, G);
+    rc |= dalloc(s, &E.g_sims, G); rc |= dalloc(s, &E.g_sel_bytes, G);
     E.cache_mask = -1;
     if (cfg->cache_capacity > 0) {
         int slots = 1;
@@ -915,6 +957,7 @@ int az_selfplay_reset(az_search* s) {
     int rc = upload_histories(s, nullptr, nullptr, nullptr, nullptr);
     if (rc) return rc;
     AZ_HIP(hipMemset(s->E.ctr, 0, sizeof(Counters)));
+    AZ_HIP(hipMemset(s->E.g_sims, 0, (size_t)s->E.G * 8));
     if (s->E.cache_mask >= 0) AZ_HIP(hipMemset(s->E.c_state, 0, (size_t)(s->E.cache_mask + 1) * sizeof(unsigned)));
     const int G = s->E.G;
     AZ_HIP(hipMemcpy(&s->E.ctr->next_game_id, &G, 4, hipMemcpyHostToDevice));
@@ -966,7 +1009,7 @@ int az_search_stats_get(az_search* s, az_search_stats* out) {
     AZ_HIP(hipStreamSynchronize(s->st));
     Counters c;
     AZ_HIP(hipMemcpy(&c, s->E.ctr, sizeof(c), hipMemcpyDeviceToHost));
-    out->sims = (int64_t)c.sims;
+    out->sims = (int64_t)(c.sims + sum_games(s, s->E.g_sims));
     out->evals = (int64_t)c.evals;
     out->terminal_leaves = (int64_t)c.terminal;
     out->games_finished = (int64_t)c.games_finished;
@@ -1013,13 +1056,12 @@ int az_search_timing(az_search* s, az_timing* out, int reset, int enable) {
     AZ_HIP(hipSetDevice(s->device));
     if (out) {
         *out = s->acc;
-        Counters c;
-        AZ_HIP(hipMemcpy(&c, s->E.ctr, sizeof(c), hipMemcpyDeviceToHost));
-        out->select_bytes = (double)c.select_bytes;
+        AZ_HIP(hipStreamSynchronize(s->st));
+        out->select_bytes = (double)sum_games(s, s->E.g_sel_bytes);
     }
     if (reset) {
         s->acc = az_timing{};
-        AZ_HIP(hipMemset(&s->E.ctr->select_bytes, 0, 8));
+        AZ_HIP(hipMemset(s->E.g_sel_bytes, 0, (size_t)s->E.G * 8));
     }
     s->timing = enable != 0;
     return 0;

@@ -72,7 +72,10 @@ constexpr int TR_SLOTS = 128;
 template <int F> struct TowerCfg;
 template <> struct TowerCfg<256> { static constexpr int BPB = 2, WB = AZ_TOWER_WB256, NCO = AZ_TOWER_NCO256; };
 template <> struct TowerCfg<128> { static constexpr int BPB = 4, WB = 1, NCO = 2; };
-template <> struct TowerCfg<64> { static constexpr int BPB = 1, WB = 1, NCO = 2; };   // C2: 256 games -> 256 workgroups
+#ifndef AZ_TOWER_NCO64
+#define AZ_TOWER_NCO64 2
+#endif
+template <> struct TowerCfg<64> { static constexpr int BPB = 1, WB = 1, NCO = AZ_TOWER_NCO64; };   // C2: 256 games -> 256 workgroups
 template <> struct TowerCfg<32> { static constexpr int BPB = 8, WB = 4, NCO = 2; };
 
 __device__ __forceinline__ float t_wave_max(float v) {
@@ -545,10 +548,29 @@ tower_kernel(const __bf16* __restrict__ planes, TowerArgs ta, const int* __restr
     const char* ldsb = reinterpret_cast<const char*>(lds);
 
     // stage the input planes [row][64][32] into H with row stride RSI
-    const uint4* src = reinterpret_cast<const uint4*>(planes) + (size_t)row0 * 64 * 4;
-    for (int c = tid; c < BPB * 64 * 4; c += NT) {
-        const int rowi = c >> 2, slot = c & 3;
-        H[rowi * RSI + slot] = rowi < nb * 64 ? src[c] : make_uint4(0, 0, 0, 0);
+    if (planes) {
+        const uint4* src = reinterpret_cast<const uint4*>(planes) + (size_t)row0 * 64 * 4;
+        for (int c = tid; c < BPB * 64 * 4; c += NT) {
+            const int rowi = c >> 2, slot = c & 3;
+            H[rowi * RSI + slot] = rowi < nb * 64 ? src[c] : make_uint4(0, 0, 0, 0);
+        }
+    } else {
+        // search mode without a planes buffer: to_tensor (chess.rs:191-245) straight from the
+        // leaf's packed position into LDS, one thread per square -- the same per-element
+        // conversion as encode_rows_kernel (net.hip), so the rows are bit-identical
+        for (int rowi = tid; rowi < BPB * 64; rowi += NT) {
+            uint4 q[4] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+            if (rowi < nb * 64) {
+                const int row = row0 + (rowi >> 6), sq = rowi & 63;
+                const azc::Pos p = so.npos[(size_t)so.row_game[row] * so.NMAX + so.row_node[row]];
+                __bf16 v[32];
+#pragma unroll
+                for (int c = 0; c < 32; c++) v[c] = (__bf16)(c < 19 ? azc::plane_value(p, c, sq) : 0.0f);
+                __builtin_memcpy(q, v, sizeof(v));
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) H[rowi * RSI + k] = q[k];
+        }
     }
     for (int c = tid; c < ZN; c += NT) lds[XSZ + HSZ + c] = make_uint4(0, 0, 0, 0);
     int* done = reinterpret_cast<int*>(lds + XSZ + HSZ + ZN);   // [8] last layer whose epilogue wave w wrote
@@ -609,6 +631,7 @@ int tower_forward(NetDev* n, const void* planes, const int* count, int rows, flo
                   const SearchOut* so, hipStream_t st) {
     if (rows <= 0) return 0;
     if (!tower_supported(n)) return fail("fused tower: unsupported net");
+    if (!planes && (!so || !so->npos)) return fail("fused tower: no planes and no leaf positions to encode");
     TowerArgs ta;
     memset(&ta, 0, sizeof(ta));
     for (int i = 0; i < 1 + 2 * n->blocks; i++) {

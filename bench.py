@@ -266,7 +266,11 @@ def main():
     peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
     conv_tflops = tm["conv_flop"] / (tm["conv_ms"] * 1e-3) / 1e12 if tm["conv_ms"] > 0 else 0.0
     tower_tflops = tm["tower_flop"] / (tm["tower_ms"] * 1e-3) / 1e12 if tm["tower_ms"] > 0 else 0.0
-    sel_gbs = tm["select_bytes"] / (tm["select_ms"] * 1e-3) / 1e9 if tm["select_ms"] > 0 else 0.0
+    # select_bytes covers every k_select launch of the window (steps x S); the event times cover
+    # the sampled launches (az_timing: every 8th simulation step)
+    sel_bytes_per_launch = tm["select_bytes"] / max(args.steps * S, 1)
+    sel_ms_per_launch = tm["select_ms"] / max(tm["select_launches"], 1)
+    sel_gbs = sel_bytes_per_launch / (sel_ms_per_launch * 1e-3) / 1e9 if tm["select_ms"] > 0 else 0.0
     out = {
         "metric": "MCTS sims/sec at 800 sims/move, 20x256 net; self-play games/hr at 1/2/4/8 GPU",
         "value": value,
@@ -290,7 +294,7 @@ def main():
                      "frac": conv_tflops / peak, "traffic": traffic,
                      "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
                      "kernel": ("tower_kernel<%d> (fused input conv + %d residual convs + heads; algorithmic "
-                                "FLOPs = conv FLOPs only), %d launches timed" % (args.filters, 2 * args.blocks,
+                                "FLOPs = conv FLOPs only), %d launches timed (HIP events on every 8th simulation step)" % (args.filters, 2 * args.blocks,
                                                                                  tm["conv_launches"]))
                                if net.fused_tower else
                                "conv3x3_kernel<%d,%d> (residual 3x3 conv), %d launches timed" %

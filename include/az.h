@@ -173,7 +173,9 @@ int az_search_stats_get(az_search* s, az_search_stats* out);
 int az_search_eval_log(az_search* s, int64_t* n_rows, int64_t* n_priors, uint64_t* keys, float* values,
                        int32_t* off, int32_t* idx, float* priors);
 
-/* Profiling: device times measured with HIP events on the engine stream while enabled.
+/* Profiling: device times measured with HIP events on the engine stream while enabled, on
+ * every 8th simulation step (steps 0, 8, 16, ...; every field except select_bytes covers
+ * those sampled steps only: sim_steps = sampled steps = select_launches).
  * conv_*: the first residual 3x3 FxF conv of every simulation step (the dominant kernel);
  * conv_flop = algorithmic FLOPs of those launches (rows * 2*64*9*F*F).  tower_*: the whole
  * conv tower.  select_bytes: algorithmic bytes read by the select walk (16 B per edge +

@@ -8,6 +8,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "../include/az.h"
 
@@ -83,8 +84,16 @@ int main(int argc, char** argv) {
             CHECK(L, L->timing(sp, &t, 0, 0));
             const double ms = t.tower_ms / (double)t.sim_steps;
             const double tf = t.tower_flop / (t.tower_ms * 1e-3) / 1e12;
-            printf("round %d  %-40s tower %.4f ms/step  %.1f TFLOP/s  sim_step %.4f ms\n", r, L->path, ms, tf,
-                   t.sim_step_ms / (double)t.sim_steps);
+            /* one more move without events: wall time per move (every kernel, gaps included) */
+            struct timespec t0, t1;
+            CHECK(L, L->sync(0));
+            clock_gettime(CLOCK_MONOTONIC, &t0);
+            CHECK(L, L->step(sp, &fin, &act));
+            CHECK(L, L->sync(0));
+            clock_gettime(CLOCK_MONOTONIC, &t1);
+            const double move_ms = (t1.tv_sec - t0.tv_sec) * 1e3 + (t1.tv_nsec - t0.tv_nsec) * 1e-6;
+            printf("round %d  %-40s tower %.4f ms/step  %.1f TFLOP/s  sim_step %.4f ms  move %.2f ms (%.0f sims/s)\n", r,
+                   L->path, ms, tf, t.sim_step_ms / (double)t.sim_steps, move_ms, games * (double)sims / (move_ms * 1e-3));
             fflush(stdout);
             if (best[i] == 0 || ms < best[i]) best[i] = ms;
             L->search_destroy(sp);
