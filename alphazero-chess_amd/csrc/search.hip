@@ -219,7 +219,7 @@ __device__ __forceinline__ int expand_leaf(const Engine& E, int g, int* nid_out)
 // branchy integer code, so fewer games per wave means less divergence and more CUs in use.
 // Row allocation and the counters are one atomic per wave (ballot + popcount), not per game.
 #ifndef AZ_EXPAND_GPW
-#define AZ_EXPAND_GPW 16
+#define AZ_EXPAND_GPW 4    // measured (tools/tower_ab): C2 4 -> 5 % faster per move than 16, 1 -> 13 % slower; C3 flat
 #endif
 __global__ void __launch_bounds__(64) k_expand(Engine E) {
     const int lane = threadIdx.x;

@@ -73,7 +73,7 @@ template <int F> struct TowerCfg;
 template <> struct TowerCfg<256> { static constexpr int BPB = 2, WB = AZ_TOWER_WB256, NCO = AZ_TOWER_NCO256; };
 template <> struct TowerCfg<128> { static constexpr int BPB = 4, WB = 1, NCO = 2; };
 #ifndef AZ_TOWER_NCO64
-#define AZ_TOWER_NCO64 2
+#define AZ_TOWER_NCO64 1   // 4 waves of 16 channels: one per SIMD (NCO 2 = 2 waves left 2 SIMDs idle: C2 tower 52 -> 41 us)
 #endif
 template <> struct TowerCfg<64> { static constexpr int BPB = 1, WB = 1, NCO = AZ_TOWER_NCO64; };   // C2: 256 games -> 256 workgroups
 template <> struct TowerCfg<32> { static constexpr int BPB = 8, WB = 4, NCO = 2; };
