@@ -58,13 +58,15 @@ static_assert(sizeof(StepRec) == 1024, "StepRec");
 
 struct Counters {                  // device-side statistics
     unsigned long long sims, evals, terminal, games_finished, moves, depth_sum, select_bytes, cache_hits;
-    int batch_count;
+    int batch_count[2];            // rows of simulation step i in [i & 1]; the backup of step i
+                                   // reads and clears it (no reset launch, and the fused step
+                                   // kernel allocates step i rows while it backs up step i - 1)
     int rec_count;
     int next_game_id;
     int log_count;
     int log_prior_count;
     int overflow;
-    int pad[2];
+    int pad[1];
 };
 
 // everything the tree kernels need, passed by value

@@ -208,6 +208,7 @@ template <class Sink> AZ_HD int gen_legal(const Pos& p, Sink& sink, bool* in_che
                               rook_att(tR, empty_xk);
     // pins and check rays from the king
     uint64_t pinned = 0, pinray[8], checkmask = checkers;
+#pragma unroll
     for (int d = 0; d < 8; d++) {
         uint64_t r = ray_dir(d, kbb, empty);
         const uint64_t sl = (d & 1) ? tB : tR;
@@ -244,8 +245,10 @@ template <class Sink> AZ_HD int gen_legal(const Pos& p, Sink& sink, bool* in_che
     };
     auto allowed = [&](int from) -> uint64_t {
         if (!((pinned >> from) & 1)) return ALL;
-        for (int d = 0; d < 8; d++) if ((pinray[d] >> from) & 1) return pinray[d];
-        return 0;
+        uint64_t r = 0;                                // pinray[] stays in registers (no early exit)
+#pragma unroll
+        for (int d = 0; d < 8; d++) r = ((pinray[d] >> from) & 1) && !r ? pinray[d] : r;
+        return r;
     };
     auto non_king = [&](uint64_t target) {
         const uint64_t ourP = p.bb[PAWN] & our;
@@ -288,6 +291,7 @@ template <class Sink> AZ_HD int gen_legal(const Pos& p, Sink& sink, bool* in_che
             uint64_t tt = knight_att(1ULL << from) & target;
             while (tt) { const int to = ctz64(tt); tt &= tt - 1; sink(move_index(from, to, us)); n++; }
         }
+#pragma unroll
         for (int role = BISHOP; role <= QUEEN; role++) {
             fr = p.bb[role] & our;
             while (fr) {

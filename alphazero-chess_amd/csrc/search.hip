@@ -20,6 +20,7 @@
 // other node (traverse_new, tree.rs:239-256), then applies Dirichlet noise
 // (tree.rs:272-289).  Nothing crosses PCIe inside a move.
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -37,14 +38,11 @@ __device__ __forceinline__ Node* game_nodes(const Engine& E, int g) { return E.n
 __device__ __forceinline__ Edge* game_edges(const Engine& E, int g) { return E.edges + (size_t)g * E.EMAX; }
 __device__ __forceinline__ azc::Pos* game_npos(const Engine& E, int g) { return E.npos + (size_t)g * E.NMAX; }
 
+__device__ __forceinline__ int* step_rows(const Engine& E, int step) { return &E.ctr->batch_count[step & 1]; }
+
 // ------------------------------------------------------------------ select
-__global__ void __launch_bounds__(256) k_select(Engine E) {
-    const int g = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-    const int lane = threadIdx.x & 63;
-    // the step's row counter restarts here (k_expand, the next kernel, allocates rows from it;
-    // the previous step's readers all ran before this launch): no memset launch per step
-    if (blockIdx.x == 0 && threadIdx.x == 0) E.ctr->batch_count = 0;
-    if (g >= E.G || !E.active[g]) return;
+// one wavefront walks game g (active) from the root to a leaf
+__device__ __forceinline__ void select_game(const Engine& E, int g, int lane) {
     const Node* nodes = game_nodes(E, g);
     const Edge* edges = game_edges(E, g);
     int* pn = E.path_node + (size_t)g * E.PMAX;
@@ -92,6 +90,12 @@ __global__ void __launch_bounds__(256) k_select(Engine E) {
     }
 }
 
+__global__ void __launch_bounds__(256) k_select(Engine E) {
+    const int g = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    if (g >= E.G || !E.active[g]) return;
+    select_game(E, g, threadIdx.x & 63);
+}
+
 // ------------------------------------------------------------------ FEN cache
 constexpr int CACHE_PROBES = 4;
 
@@ -102,9 +106,9 @@ __device__ __forceinline__ bool same_fen(const azc::Pos& a, const azc::Pos& b) {
 }
 
 // insert every row just evaluated by the network (process_batch's cache.insert, training.rs:413)
-__global__ void __launch_bounds__(64) k_cache_insert(Engine E) {
+__global__ void __launch_bounds__(64) k_cache_insert(Engine E, int step) {
     const int row = blockIdx.x * blockDim.x + threadIdx.x;
-    if (row >= E.ctr->batch_count) return;
+    if (row >= *step_rows(E, step)) return;
     const int g = E.row_game[row], node = E.row_node[row];
     const azc::Pos p = E.npos[(size_t)g * E.NMAX + node];
     const Node nd = E.nodes[(size_t)g * E.NMAX + node];
@@ -221,7 +225,7 @@ __device__ __forceinline__ int expand_leaf(const Engine& E, int g, int* nid_out)
 #ifndef AZ_EXPAND_GPW
 #define AZ_EXPAND_GPW 4    // measured (tools/tower_ab): C2 4 -> 5 % faster per move than 16, 1 -> 13 % slower; C3 flat
 #endif
-__global__ void __launch_bounds__(64) k_expand(Engine E) {
+__global__ void __launch_bounds__(64) k_expand(Engine E, int step) {
     const int lane = threadIdx.x;
     const int g = lane < AZ_EXPAND_GPW ? blockIdx.x * AZ_EXPAND_GPW + lane : E.G;
     int nid = -1;
@@ -230,7 +234,7 @@ __global__ void __launch_bounds__(64) k_expand(Engine E) {
     if (mrow) {
         const int leader = __builtin_ctzll(mrow);
         int base = 0;
-        if (lane == leader) base = atomicAdd(&E.ctr->batch_count, __popcll(mrow));
+        if (lane == leader) base = atomicAdd(step_rows(E, step), __popcll(mrow));
         base = __shfl(base, leader, 64);
         if (kind == X_ROW) {
             const int row = base + __popcll(mrow & ((1ull << lane) - 1ull));
@@ -245,14 +249,18 @@ __global__ void __launch_bounds__(64) k_expand(Engine E) {
 }
 
 // ------------------------------------------------------------------ backup
-__global__ void __launch_bounds__(256) k_backup(Engine E, int step) {
-    const int g = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-    const int lane = threadIdx.x & 63;
-    if (g == 0 && lane == 0) {
-        atomicAdd(&E.ctr->evals, (unsigned long long)E.ctr->batch_count);
-        if (step >= 0 && step < E.S) E.batch_hist[step] = E.ctr->batch_count;
-    }
-    if (g >= E.G || !E.active[g]) return;
+// the step's statistics (one thread of the grid): rows evaluated, then the row counter is
+// cleared for step + 2
+__device__ __forceinline__ void backup_stats(const Engine& E, int step) {
+    int* rows = step_rows(E, step);
+    const int n = *rows;
+    atomicAdd(&E.ctr->evals, (unsigned long long)n);
+    if (step >= 0 && step < E.S) E.batch_hist[step] = n;
+    *rows = 0;
+}
+
+// one wavefront backs up game g (active), one lane per tree level
+__device__ __forceinline__ void backup_game(const Engine& E, int g, int lane) {
     Node* nodes = game_nodes(E, g);
     Edge* edges = game_edges(E, g);
     const int kind = E.leaf_kind[g], len = E.leaf_len[g];
@@ -268,6 +276,62 @@ __global__ void __launch_bounds__(256) k_backup(Engine E, int step) {
         nodes[pn[k]].nsum += 1;
     }
     if (lane == 0) E.g_sims[g] += 1ull;                         // per-game slot, summed at readout
+}
+
+__global__ void __launch_bounds__(256) k_backup(Engine E, int step) {
+    const int g = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const int lane = threadIdx.x & 63;
+    if (g == 0 && lane == 0) backup_stats(E, step);
+    if (g >= E.G || !E.active[g]) return;
+    backup_game(E, g, lane);
+}
+
+// ------------------------------------------------------------------ fused step
+// One launch per simulation step instead of three: backup of step `bstep` (the previous one,
+// or none when < 0), then select and expand of step `step`, one wavefront per game (the
+// expansion on lane 0).  A game's backup, select and expand touch only that game's tree, so
+// the wave needs no grid-wide order; the wave's own global stores (backup) are made visible
+// to its later loads (select) by a workgroup-scope fence.  Rows are allocated with one atomic
+// per workgroup (STEP_WPB games).  bstep's row counter is read and cleared by one thread;
+// step's counter (the other parity) was cleared by the backup of step - 2.
+constexpr int STEP_WPB = 4;     // 256 threads: the expansion needs ~180 VGPRs and its 80-B position stays in registers only up to this size
+__global__ void __launch_bounds__(STEP_WPB * 64) k_step(Engine E, int step, int bstep) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int g = blockIdx.x * STEP_WPB + w;
+    __shared__ int s_kind[STEP_WPB], s_nid[STEP_WPB], s_base;
+    const bool live = g < E.G && E.active[g];
+    if (bstep >= 0) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) backup_stats(E, bstep);
+        if (live) backup_game(E, g, lane);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    }
+    int kind = X_NONE, nid = -1;
+    if (live) {
+        select_game(E, g, lane);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        if (lane == 0) kind = expand_leaf(E, g, &nid);
+    }
+    if (lane == 0) { s_kind[w] = kind; s_nid[w] = nid; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int nr = 0, nt = 0, nc = 0;
+        for (int i = 0; i < STEP_WPB; i++) {
+            nr += s_kind[i] == X_ROW;
+            nt += s_kind[i] == X_TERMINAL;
+            nc += s_kind[i] == X_CACHED;
+        }
+        s_base = nr ? atomicAdd(step_rows(E, step), nr) : 0;
+        if (nt) atomicAdd(&E.ctr->terminal, (unsigned long long)nt);
+        if (nc) atomicAdd(&E.ctr->cache_hits, (unsigned long long)nc);
+    }
+    __syncthreads();
+    if (lane == 0 && kind == X_ROW) {
+        int row = s_base;
+        for (int i = 0; i < w; i++) row += s_kind[i] == X_ROW;
+        E.row_game[row] = g;
+        E.row_node[row] = nid;
+        E.leaf_row[g] = row;
+    }
 }
 
 // ------------------------------------------------------------------ roots
@@ -287,7 +351,7 @@ __global__ void __launch_bounds__(64) k_root_setup(Engine E) {
     E.node_count[g] = 1;
     E.edge_count[g] = n;
     E.max_depth[g] = 0;
-    const int row = atomicAdd(&E.ctr->batch_count, 1);
+    const int row = atomicAdd(&E.ctr->batch_count[0], 1);   // cleared again after the root eval
     E.row_game[row] = g;
     E.row_node[row] = 0;
 }
@@ -541,6 +605,9 @@ __global__ void k_readout(Engine E, float* improved, uint32_t* visits, int* dept
 }  // namespace azi
 
 // ====================================================================== host engine
+#ifndef AZ_FUSED_STEPS
+#define AZ_FUSED_STEPS 1
+#endif
 using namespace azi;
 
 struct az_search {
@@ -558,6 +625,7 @@ struct az_search {
     bool roots_fresh = false;        // trees sized for exactly S sims per root
     // timing
     bool timing = false;
+    bool fused_steps = AZ_FUSED_STEPS != 0;   // k_step (backup + select + expand in one launch); env AZ_FUSED_STEPS=0: separate kernels
     std::vector<hipEvent_t> ev;      // 7 per sim step
     az_timing acc{};
 };
@@ -586,16 +654,12 @@ unsigned long long sum_games(az_search* s, const unsigned long long* d) {
     return t;
 }
 
-int sim_step(az_search* s, int step, hipEvent_t* ev) {
+// network evaluation of step `step`'s rows (+ FEN cache insert); events 3, 7, 8, 4 when timed
+int eval_step(az_search* s, int step, hipEvent_t* ev) {
     Engine& E = s->E;
     hipStream_t st = s->st;
     const int G = E.G;
-    if (ev) (void)hipEventRecord(ev[0], st);
-    k_select<<<(G * 64 + 255) / 256, 256, 0, st>>>(E);
-    if (ev) (void)hipEventRecord(ev[1], st);
-    k_expand<<<(G + AZ_EXPAND_GPW - 1) / AZ_EXPAND_GPW, 64, 0, st>>>(E);
-    if (ev) (void)hipEventRecord(ev[2], st);
-    const int* cnt = &E.ctr->batch_count;
+    const int* cnt = &E.ctr->batch_count[step & 1];
     int rc = 0;
     if (s->cfg.evaluator == AZ_EVAL_NET) {
         NetDev* n = s->net->dev;
@@ -623,17 +687,42 @@ int sim_step(az_search* s, int step, hipEvent_t* ev) {
         rc = synth_eval_rows(cnt, G, s->so, st);
         if (rc) return rc;
     }
-    if (E.cache_mask >= 0) k_cache_insert<<<(G + 63) / 64, 64, 0, st>>>(E);
+    if (E.cache_mask >= 0) k_cache_insert<<<(G + 63) / 64, 64, 0, st>>>(E, step);
+    return 0;
+}
+
+// one simulation step as separate kernels, bracketed by events when timed
+int sim_step(az_search* s, int step, hipEvent_t* ev) {
+    Engine& E = s->E;
+    hipStream_t st = s->st;
+    const int G = E.G;
+    if (ev) (void)hipEventRecord(ev[0], st);
+    k_select<<<(G * 64 + 255) / 256, 256, 0, st>>>(E);
+    if (ev) (void)hipEventRecord(ev[1], st);
+    k_expand<<<(G + AZ_EXPAND_GPW - 1) / AZ_EXPAND_GPW, 64, 0, st>>>(E, step);
+    if (ev) (void)hipEventRecord(ev[2], st);
+    int rc = eval_step(s, step, ev);
+    if (rc) return rc;
     if (ev) (void)hipEventRecord(ev[5], st);
     k_backup<<<(G * 64 + 255) / 256, 256, 0, st>>>(E, step);
     if (ev) (void)hipEventRecord(ev[6], st);
     return hipGetLastError() == hipSuccess ? 0 : fail("sim step launch failed");
 }
 
+// one simulation step through the fused kernel: backup of bstep (< 0: none), select + expand
+// of step, then the evaluation; step's own backup is left to the next launch
+int sim_step_fused(az_search* s, int step, int bstep) {
+    Engine& E = s->E;
+    k_step<<<(E.G + STEP_WPB - 1) / STEP_WPB, STEP_WPB * 64, 0, s->st>>>(E, step, bstep);
+    int rc = eval_step(s, step, nullptr);
+    if (rc) return rc;
+    return hipGetLastError() == hipSuccess ? 0 : fail("sim step launch failed");
+}
+
 // evaluation of batch rows set up by k_root_setup (rows = games)
 int eval_rows(az_search* s) {
     Engine& E = s->E;
-    const int* cnt = &E.ctr->batch_count;
+    const int* cnt = &E.ctr->batch_count[0];
     if (s->cfg.evaluator == AZ_EVAL_NET) {
         NetDev* n = s->net->dev;
         if (n->fused && tower_supported(n)) return tower_forward(n, nullptr, cnt, E.G, nullptr, nullptr, &s->so, s->st);
@@ -656,11 +745,24 @@ int run_sims(az_search* s) {
         }
     }
     // timing mode brackets every TIMING_EVERY-th simulation step with events (an event record
-    // costs a few us of GPU time: on every step it was ~20 % of a 6x64 simulation step)
+    // costs a few us of GPU time: on every step it was ~20 % of a 6x64 simulation step); those
+    // steps run as separate kernels, the others through the fused step kernel
+    int pending = -1;                  // step whose backup is still to launch
     for (int i = 0; i < S; i++) {
-        int rc = sim_step(s, i, tm && i % TIMING_EVERY == 0 ? &s->ev[EV_PER_STEP * i] : nullptr);
+        const bool timed = tm && i % TIMING_EVERY == 0;
+        int rc;
+        if (timed || !s->fused_steps) {
+            if (pending >= 0) k_backup<<<(s->E.G * 64 + 255) / 256, 256, 0, s->st>>>(s->E, pending);
+            pending = -1;
+            rc = sim_step(s, i, timed ? &s->ev[EV_PER_STEP * i] : nullptr);
+        } else {
+            rc = sim_step_fused(s, i, pending);
+            pending = i;
+        }
         if (rc) return rc;
     }
+    if (pending >= 0) k_backup<<<(s->E.G * 64 + 255) / 256, 256, 0, s->st>>>(s->E, pending);
+    AZ_HIP(hipGetLastError());
     if (tm) {
         AZ_HIP(hipStreamSynchronize(s->st));
         std::vector<int> rows(S);
@@ -735,10 +837,11 @@ int upload_histories(az_search* s, const int32_t* hist, const int32_t* off, cons
 
 int setup_roots(az_search* s, int apply_noise, bool save_template) {
     Engine& E = s->E;
-    AZ_HIP(hipMemsetAsync(&E.ctr->batch_count, 0, sizeof(int), s->st));
+    AZ_HIP(hipMemsetAsync(E.ctr->batch_count, 0, sizeof(E.ctr->batch_count), s->st));
     k_root_setup<<<(E.G + 63) / 64, 64, 0, s->st>>>(E);
     int rc = eval_rows(s);
     if (rc) return rc;
+    AZ_HIP(hipMemsetAsync(E.ctr->batch_count, 0, sizeof(int), s->st));   // simulation step 0 allocates from [0]
     if (save_template) k_save_start_template<<<1, 256, 0, s->st>>>(E);
     k_root_noise<<<E.G, 64, 0, s->st>>>(E, apply_noise);
     AZ_HIP(hipGetLastError());
@@ -817,6 +920,7 @@ int az_search_create(az_net* net, const az_search_cfg* cfg, int device, az_searc
     s->cfg = *cfg;
     s->device = device;
     s->net = net;
+    if (const char* v = getenv("AZ_FUSED_STEPS")) s->fused_steps = atoi(v) != 0;   // A/B and parity tests
     AZ_HIP(hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking));
     Engine& E = s->E;
     const int G = cfg->games, S = cfg->sims;

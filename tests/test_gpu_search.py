@@ -168,3 +168,25 @@ def test_search_survives_nan_network(require_gpu):
     imp, vis, dep = s.run()
     assert np.all(vis.sum(axis=1) == 64)
     assert np.all((dep >= 1) & (dep <= 64))
+
+
+@pytest.mark.parametrize("cache", [0, 1 << 16])
+def test_fused_step_kernel_matches_separate_kernels(require_gpu, monkeypatch, cache):
+    """k_step (backup of step i-1 + select + expand of step i in one launch) against the
+    separate k_select / k_expand / k_backup launches, and against the timed mix (every 8th
+    step separate): identical games, visit counts, evaluations and cache hits."""
+    net = A.AlphaZero(2, 32, dtype="bf16")
+    runs = []
+    for fused, timing in ((True, False), (False, False), (True, True)):
+        monkeypatch.setenv("AZ_FUSED_STEPS", "1" if fused else "0")
+        sp = A.SelfPlay(net, games=12, sims=40, seed=13, cache_capacity=cache)
+        sp.reset()
+        sp.search.timing(reset=True, enable=timing)
+        for _ in range(6):
+            sp.step()
+        st = sp.search.stats()
+        runs.append(((st["sims"], st["evals"], st["terminal_leaves"], st["cache_hits"]),
+                     sorted((s.game_id, s.ply, s.action, s.search_depth, tuple(sorted(s.visits.items())))
+                            for s in sp.drain())))
+    assert runs[0][0][0] == 12 * 40 * 6
+    assert runs[0] == runs[1] == runs[2]
