@@ -177,7 +177,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-games", type=int, default=16)
-    ap.add_argument("--cpu-sims", type=int, default=8)
+    ap.add_argument("--cpu-sims", type=int, default=32, help="sims per sampled search (~12 s of host work at 20x256)")
     ap.add_argument("--train-steps", type=int, default=5, help="timed training steps (0 = skip the training phase)")
     ap.add_argument("--train-batch", type=int, default=512, help="positions per rank (BATCH_SIZE, parameters.rs:17)")
     ap.add_argument("--train-timeout", type=int, default=240)
