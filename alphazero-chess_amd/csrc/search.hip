@@ -157,9 +157,18 @@ __device__ __forceinline__ int expand_leaf(const Engine& E, int g, int* nid_out)
     Edge* edges = game_edges(E, g);
     azc::Pos* npos = game_npos(E, g);
     const int parent = E.leaf_node[g], eabs = E.leaf_edge[g];
+    // every per-game word the expansion needs is loaded up front: issued together, and ahead
+    // of the edge stores below, behind which the compiler would otherwise order them
     const int idx = edges[eabs].idx & azc::IDX_MASK;
-    azc::Pos c = azc::play_index(npos[parent], idx);
+    const azc::Pos pp = npos[parent];
     const int ebeg = E.edge_count[g];
+    const int nid = E.node_count[g];
+    const int pdepth = nodes[parent].depth;
+    const int maxd = E.max_depth[g];
+    const int hlen = E.hist_len[g];
+    const int plen = E.leaf_len[g];                           // select's root -> parent path
+    const int* pn = E.path_node + (size_t)g * E.PMAX;
+    azc::Pos c = azc::play_index(pp, idx);
     EdgeSink sink{edges + ebeg, 0};
     bool chk = false, lep = false;
     const int n = azc::gen_legal(c, sink, &chk, &lep);
@@ -167,15 +176,16 @@ __device__ __forceinline__ int expand_leaf(const Engine& E, int g, int* nid_out)
     c.rep_key = azc::rep_key_of(c);
     int res = azc::outcome(c, n, chk);                       // chess.rs:43-50
     if (res == azc::ONGOING) {                               // chess.rs:52-60
-        int cnt = 0, d = 1, cur = parent;
+        // positions d plies back (d even: same side to move), d <= halfmoves: first the tree
+        // path (pn[plen - d], independent loads instead of a parent-pointer chase), then history
+        int cnt = 0;
         const int hm = c.halfmoves;
-        while (cur >= 0 && d <= hm) {
-            if (!(d & 1) && azc::chess_eq(npos[cur], c)) cnt++;
-            cur = nodes[cur].parent;
-            d++;
-        }
+        const int dt = hm < plen ? hm : plen;
+        for (int d2 = 2; d2 <= dt; d2 += 2)
+            if (azc::chess_eq(npos[pn[plen - d2]], c)) cnt++;
+        int d = plen + 1;
         const azc::Pos* hist = E.hist + (size_t)g * HMAX;
-        for (int hi = E.hist_len[g] - 2; hi >= 0 && d <= hm; hi--, d++)
+        for (int hi = hlen - 2; hi >= 0 && d <= hm; hi--, d++)
             if (!(d & 1) && azc::chess_eq(hist[hi], c)) cnt++;
         if (cnt + 1 >= azc::REPETITIONS || c.halfmoves >= azc::NUM_HALFMOVES || c.fullmoves >= azc::NUM_FULLMOVES)
             res = azc::DRAW;
@@ -185,7 +195,6 @@ __device__ __forceinline__ int expand_leaf(const Engine& E, int g, int* nid_out)
         E.leaf_kind[g] = res == azc::DRAW ? LEAF_DRAW : LEAF_WIN;
         return X_TERMINAL;
     }
-    const int nid = E.node_count[g];
     if (nid >= E.NMAX || ebeg + n > E.EMAX) {                // cannot happen with NMAX = S + 2
         E.leaf_kind[g] = LEAF_DRAW;
         atomicAdd(&E.ctr->overflow, 1);
@@ -194,7 +203,7 @@ __device__ __forceinline__ int expand_leaf(const Engine& E, int g, int* nid_out)
     Node nn;
     nn.edge_begin = (uint32_t)ebeg;
     nn.nedges = (uint16_t)n;
-    nn.depth = (uint16_t)(nodes[parent].depth + 1);
+    nn.depth = (uint16_t)(pdepth + 1);
     nn.nsum = 0;
     nn.parent = parent;
     nodes[nid] = nn;
@@ -202,7 +211,7 @@ __device__ __forceinline__ int expand_leaf(const Engine& E, int g, int* nid_out)
     E.node_count[g] = nid + 1;
     E.edge_count[g] = ebeg + n;
     edges[eabs].child = nid;
-    if (nn.depth > E.max_depth[g]) E.max_depth[g] = nn.depth;
+    if (nn.depth > maxd) E.max_depth[g] = nn.depth;
     if (E.cache_mask >= 0) {                                 // FEN cache lookup (tree.rs:214-219)
         const uint64_t key = azc::fen_key(c);
         for (int i = 0; i < CACHE_PROBES; i++) {
