@@ -13,6 +13,9 @@
 //             encode -> conv tower -> fused heads writing legal priors into the edges;
 //   k_backup  (1 wavefront / game, one lane per tree level): W += +-v, N += 1
 //             (tree.rs:134-143, 197-206).
+// Outside the timed (event-bracketed) steps the three tree kernels run as ONE launch,
+// k_step: backup of step i-1, select and expand of step i, one wavefront per game (the
+// expansion on its lane 0), so a simulation step is two launches: k_step and the tower.
 // A move step (k_finish) computes the improved policy visits/sum (tree.rs:110-114),
 // chooses the action (argmax with the LAST max at fullmoves >= 15, else WeightedIndex
 // over f32 cumulative sums: training.rs:310-321), records the EpisodeStep, plays it and

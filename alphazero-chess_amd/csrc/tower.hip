@@ -37,6 +37,9 @@
 #ifndef AZ_TOWER_LA
 #define AZ_TOWER_LA 4      // activation (B-fragment) LDS reads issued this many fragments ahead
 #endif
+#ifndef AZ_HEADS_KPRE
+#define AZ_HEADS_KPRE 64   // value-FC rows per wave prefetched into registers before the 1x1 conv
+#endif
 #ifndef AZ_TOWER_PF
 #define AZ_TOWER_PF 2      // weight prefetch depth in k-steps (L2 latency cover; 4 measured no faster)
 #endif
@@ -338,7 +341,7 @@ __device__ __forceinline__ void heads_group(const char* __restrict__ xb, float* 
     float* stat = scr + S::STAT;                        // per board: [NW] max, [NW] sum, value, slot, prior off
     // weights of B and C are fetched into registers first: their latency hides behind A
     constexpr int TPW = 16 * NB / NW;                   // policy tiles per wave
-    constexpr int KP = 512 / NW, KPRE = KP < 64 ? KP : 64;
+    constexpr int KP = 512 / NW, KPRE = KP < AZ_HEADS_KPRE ? KP : AZ_HEADS_KPRE;
     float pa[TPW > 0 ? TPW : 1][8];
 #pragma unroll
     for (int k = 0; k < TPW; k++) {
@@ -346,7 +349,7 @@ __device__ __forceinline__ void heads_group(const char* __restrict__ xb, float* 
 #pragma unroll
         for (int ks = 0; ks < 8; ks++) pa[k][ks] = head[L.p2w + (cf * 16 + l16) * 32 + h + ks * 4];
     }
-    float wv[KPRE];
+    float wv[KPRE > 0 ? KPRE : 1];
 #pragma unroll
     for (int i = 0; i < KPRE; i++) wv[i] = head[L.l1w + (size_t)(w * KP + i) * 64 + lane];
     // A
