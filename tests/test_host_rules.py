@@ -23,6 +23,7 @@ EDGE_FENS = [
     "3k4/8/8/8/8/8/8/3KQ3 b - - 99 150",
     "7k/6Q1/6K1/8/8/8/8/8 b - - 0 1",             # checkmate
     "7k/5Q2/6K1/8/8/8/8/8 b - - 0 1",             # stalemate
+    "R6R/3Q4/1Q4Q1/4Q3/2Q4Q/Q4Q2/pp1Q4/kBNN1KB1 w - - 0 1",   # 218 legal moves: the maximum (MAX_EDGES)
 ]
 
 
