@@ -37,6 +37,9 @@
 #ifndef AZ_TOWER_LA
 #define AZ_TOWER_LA 4      // activation (B-fragment) LDS reads issued this many fragments ahead
 #endif
+#ifndef AZ_TOWER_PAIRW
+#define AZ_TOWER_PAIRW 0   // 1: explicit LDS wait per pair of activation fragments (fewer s_waitcnt in the MFMA stream)
+#endif
 #ifndef AZ_HEADS_KPRE
 #define AZ_HEADS_KPRE 64   // value-FC rows per wave prefetched into registers before the 1x1 conv
 #endif
@@ -227,6 +230,11 @@ __device__ __forceinline__ void conv_lds(const char* __restrict__ ldsb, uint4* _
                 const bool last_of_group = tap == 8 && c4 + 1 == CPH && half + 1 < NSPLIT;
 #pragma unroll
                 for (int m = 0; m < MF; m++) {
+#if AZ_TOWER_PAIRW
+                    // one LDS wait per fragment pair (fragments m, m+1 done: LA-2 reads left in
+                    // flight); the compiler's own per-fragment waits become redundant and drop
+                    if ((m & 1) == 0) __builtin_amdgcn_s_waitcnt(0xC07F & ~0x0F00 | ((LA - 2) << 8));
+#endif
                     const uint4 bv = bq[m % LA];
 #ifndef AZ_TOWER_NOLDSR   // (experiment only: no activation reads inside the loop)
                     if (m + LA < MF) {
