@@ -37,6 +37,10 @@
 #ifndef AZ_TOWER_LA
 #define AZ_TOWER_LA 4      // activation (B-fragment) LDS reads issued this many fragments ahead
 #endif
+#ifndef AZ_TOWER_ADAPT
+#define AZ_TOWER_ADAPT 1   // N > 0: N times per tap, issue priority to whichever wave of a SIMD pair is behind
+                           // (A/B at C3: 1 = -1.0 % and -1.2 % tower time, 2 = +1.8 %, 4 = +3.9 %, 8 = +13 %)
+#endif
 #ifndef AZ_TOWER_PAIRW
 #define AZ_TOWER_PAIRW 0   // 1: explicit LDS wait per pair of activation fragments (fewer s_waitcnt in the MFMA stream)
 #endif
@@ -133,7 +137,8 @@ __device__ __forceinline__ void conv_lds(const char* __restrict__ ldsb, uint4* _
                                          int zero_off, const uint4* __restrict__ wsw, const uint4* __restrict__ wnext,
                                          const float* __restrict__ bias, uint4 (&wr)[RingPF<CIN / 32>::PF][NCO],
                                          int cw, int bw, int lane, int wpar, unsigned long long* trw = nullptr,
-                                         int* done = nullptr, int lidx = 0) {
+                                         int* done = nullptr, int lidx = 0, int* prog = nullptr, int wid = 0,
+                                         int partner = -1) {
     constexpr int NCH = CIN / 32;                     // 32-channel K chunks (4 slots)
     if (trw && lane == 0) trw[0] = __builtin_amdgcn_s_memtime();
 #ifdef AZ_TOWER_SOLO   // experiment only: waves 4-7 skip the residual convs (waves 0-3 run alone on their SIMDs)
@@ -200,11 +205,28 @@ __device__ __forceinline__ void conv_lds(const char* __restrict__ ldsb, uint4* _
         tap_bases(0, bcur);
 #pragma unroll
         for (int m = 0; m < LA; m++) bq[m] = *reinterpret_cast<const uint4*>(ldsb + bcur[m] + half * CPH * 64);
+#if AZ_TOWER_ADAPT
+        // progress-based issue priority between the two waves of a SIMD: the wave that is
+        // behind its partner (by the partner's tap count read one tap earlier) issues first,
+        // so both reach the layer barrier together instead of one finishing alone
+        constexpr int ACH = AZ_TOWER_ADAPT < CPH ? AZ_TOWER_ADAPT : CPH;   // checks per tap
+        constexpr bool ADAPT = F == 256 && CIN == F;  // two waves per SIMD (C2's 4-wave tower: +5 % without this guard)
+        int other = lidx * 9 * ACH;
+#endif
         for (int tap = 0; tap < 9; tap++) {
             tap_bases(tap < 8 ? tap + 1 : 8, bnext);
 #pragma unroll
             for (int c4 = 0; c4 < CPH; c4++) {
                 const int cc = half * CPH + c4;
+#if AZ_TOWER_ADAPT
+                if (ADAPT && partner >= 0 && c4 % (CPH / ACH) == 0) {
+                    const int mine = (lidx * 9 + tap) * ACH + c4 / (CPH / ACH);
+                    if (lane == 0) *reinterpret_cast<volatile int*>(prog + wid) = mine;
+                    if (mine > other) __builtin_amdgcn_s_setprio(0);
+                    else __builtin_amdgcn_s_setprio(1);
+                    other = __builtin_amdgcn_readfirstlane(*reinterpret_cast<volatile int*>(prog + partner));
+                }
+#endif
                 if constexpr (AZ_TOWER_PRIO > 0) {
                     if ((((cc / AZ_TOWER_PRIO) & 1) ^ wpar) != 0) __builtin_amdgcn_s_setprio(1);
                     else __builtin_amdgcn_s_setprio(0);
@@ -275,7 +297,7 @@ __device__ __forceinline__ void conv_lds(const char* __restrict__ ldsb, uint4* _
     // the compiler does not see the asm MFMAs: cover the XDL-write -> VALU-read hazard by hand
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 #endif
-    if constexpr (AZ_TOWER_PRIO > 0) __builtin_amdgcn_s_setprio(0);
+    if constexpr (AZ_TOWER_PRIO > 0 || (AZ_TOWER_ADAPT && F == 256 && CIN == F)) __builtin_amdgcn_s_setprio(0);
     if (trw && lane == 0) trw[1] = __builtin_amdgcn_s_memtime();
     // `in` and `out` are different buffers, so the epilogue needs no barrier before it;
     // the barrier after it publishes `out` to the next layer.
@@ -525,7 +547,7 @@ tower_kernel(const __bf16* __restrict__ planes, TowerArgs ta, const int* __restr
     constexpr int HSZ = ((XSZ > HSZ0 ? XSZ : HSZ0) + 15) / 16 * 16;
     // chunk-group split + per-wave done flags (no barrier between residual convs): F = 256 only
     constexpr int NSP = (AZ_TOWER_FLAGS && F == 256 && WB == 1) ? 2 : 1;
-    __shared__ __attribute__((aligned(16))) uint4 lds[XSZ + HSZ + ZN + 2];
+    __shared__ __attribute__((aligned(16))) uint4 lds[XSZ + HSZ + ZN + 6];
     const int count = count_ptr ? min(*count_ptr, rows) : rows;
     const int row0 = blockIdx.x * BPB;
     if (row0 >= count) return;
@@ -586,8 +608,27 @@ tower_kernel(const __bf16* __restrict__ planes, TowerArgs ta, const int* __restr
     for (int c = tid; c < ZN; c += NT) lds[XSZ + HSZ + c] = make_uint4(0, 0, 0, 0);
     int* done = reinterpret_cast<int*>(lds + XSZ + HSZ + ZN);   // [8] last layer whose epilogue wave w wrote
     if (tid < 8) done[tid] = 0;                              // layer 0 = the input conv (barrier after it)
+    int* prog = done + 8;                                    // [8] tap counter per wave, [8] its SIMD
+#if AZ_TOWER_ADAPT
+    if constexpr (F == 256) {
+        unsigned hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        if (lane == 0) { prog[8 + (tid >> 6)] = (hw >> 4) & 3; prog[tid >> 6] = 0; }
+    }
+#endif
     __syncthreads();
     TR_STAMP(1);
+    int partner = -1;                                        // the other wave on this wave's SIMD
+#if AZ_TOWER_ADAPT
+    if constexpr (F == 256) {
+        const int me = __builtin_amdgcn_readfirstlane(tid >> 6);
+        int nsame = 0;
+        for (int i = 0; i < NT / 64; i++)
+            if (i != me && prog[8 + i] == prog[8 + me]) { partner = i; nsame++; }
+        if (nsame != 1) partner = -1;                        // not exactly two waves on the SIMD
+        partner = __builtin_amdgcn_readfirstlane(partner);
+    }
+#endif
     {
         uint4 wr0[RingPF<1>::PF][NCO];
         ring_fill<1, F, NCO>(wr0, ta.w[0], cw, lane);
@@ -605,10 +646,11 @@ tower_kernel(const __bf16* __restrict__ planes, TowerArgs ta, const int* __restr
         unsigned long long* trw = nullptr;
 #endif
         conv_lds<F, RSF, F, RSF, BPW, NCO, false, NSP>(ldsb, H, 0, zero_off, ta.w[1 + 2 * b], ta.w[2 + 2 * b],
-                                                       ta.b[1 + 2 * b], wr, cw, bw, lane, wpar, trw, done, 1 + 2 * b);
+                                                       ta.b[1 + 2 * b], wr, cw, bw, lane, wpar, trw, done, 1 + 2 * b,
+                                                       prog, w, partner);
         conv_lds<F, RSF, F, RSF, BPW, NCO, true, NSP>(ldsb, X, XSZ * 16, zero_off, ta.w[2 + 2 * b], after,
                                                       ta.b[2 + 2 * b], wr, cw, bw, lane, wpar,
-                                                      trw ? trw + 4 : nullptr, done, 2 + 2 * b);
+                                                      trw ? trw + 4 : nullptr, done, 2 + 2 * b, prog, w, partner);
         TR_STAMP(3 + b);
     }
     if constexpr (NSP > 1) __syncthreads();           // the heads read every channel
