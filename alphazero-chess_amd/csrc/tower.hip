@@ -221,10 +221,13 @@ __device__ __forceinline__ void conv_lds(const char* __restrict__ ldsb, uint4* _
 #if AZ_TOWER_ADAPT
                 if (ADAPT && partner >= 0 && c4 % (CPH / ACH) == 0) {
                     const int mine = (lidx * 9 + tap) * ACH + c4 / (CPH / ACH);
-                    if (lane == 0) *reinterpret_cast<volatile int*>(prog + wid) = mine;
+                    // LDS-typed accesses: through the generic pointer they compile to flat ops,
+                    // which count against vmcnt too and stall the weight-prefetch waits
+                    typedef __attribute__((address_space(3))) volatile int lds_vint;
+                    if (lane == 0) *(lds_vint*)(prog + wid) = mine;
                     if (mine > other) __builtin_amdgcn_s_setprio(0);
                     else __builtin_amdgcn_s_setprio(1);
-                    other = __builtin_amdgcn_readfirstlane(*reinterpret_cast<volatile int*>(prog + partner));
+                    other = __builtin_amdgcn_readfirstlane(*(lds_vint*)(prog + partner));
                 }
 #endif
                 if constexpr (AZ_TOWER_PRIO > 0) {
