@@ -41,6 +41,10 @@
 #define AZ_TOWER_ADAPT 1   // N > 0: N times per tap, issue priority to whichever wave of a SIMD pair is behind
                            // (A/B at C3: 1 = -1.0 % and -1.2 % tower time, 2 = +1.8 %, 4 = +3.9 %, 8 = +13 %)
 #endif
+#ifndef AZ_TOWER_TAPU
+#define AZ_TOWER_TAPU 9    // tap-loop unroll factor: 9 (full) = per-tap offsets and validity at compile time, no
+                           // loop-carried register copies (C3 A/B: tower -2.7 %; 3 = neutral)
+#endif
 #ifndef AZ_TOWER_PAIRW
 #define AZ_TOWER_PAIRW 0   // 1: explicit LDS wait per pair of activation fragments (fewer s_waitcnt in the MFMA stream)
 #endif
@@ -213,6 +217,7 @@ __device__ __forceinline__ void conv_lds(const char* __restrict__ ldsb, uint4* _
         constexpr bool ADAPT = F == 256 && CIN == F;  // two waves per SIMD (C2's 4-wave tower: +5 % without this guard)
         int other = lidx * 9 * ACH;
 #endif
+#pragma unroll AZ_TOWER_TAPU
         for (int tap = 0; tap < 9; tap++) {
             tap_bases(tap < 8 ? tap + 1 : 8, bnext);
 #pragma unroll
