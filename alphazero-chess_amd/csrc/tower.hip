@@ -38,8 +38,9 @@
 #define AZ_TOWER_LA 4      // activation (B-fragment) LDS reads issued this many fragments ahead
 #endif
 #ifndef AZ_TOWER_ADAPT
-#define AZ_TOWER_ADAPT 1   // N > 0: N times per tap, issue priority to whichever wave of a SIMD pair is behind
-                           // (A/B at C3: 1 = -1.0 % and -1.2 % tower time, 2 = +1.8 %, 4 = +3.9 %, 8 = +13 %)
+#define AZ_TOWER_ADAPT 0   // N > 0: N times per tap, issue priority to whichever wave of a SIMD pair is behind
+                           // (rolled tap loop: 1 = -1.0 % / -1.2 % tower time, 2 = +1.8 %, 4 = +3.9 %, 8 = +13 %;
+                           // with the unrolled loop, 1 = +0.4 ... +1.5 %: off)
 #endif
 #ifndef AZ_TOWER_TAPU
 #define AZ_TOWER_TAPU 9    // tap-loop unroll factor: 9 (full) = per-tap offsets and validity at compile time, no
