@@ -46,6 +46,9 @@
 #define AZ_TOWER_TAPU 9    // tap-loop unroll factor: 9 (full) = per-tap offsets and validity at compile time, no
                            // loop-carried register copies (C3 A/B: tower -2.7 %; 3 = neutral)
 #endif
+#ifndef AZ_TOWER_BUFW
+#define AZ_TOWER_BUFW 1    // 1: weight refills as buffer loads (SGPR descriptor + k-step SGPR offset): C3 A/B tower -2.7 %
+#endif
 #ifndef AZ_TOWER_PAIRW
 #define AZ_TOWER_PAIRW 0   // 1: explicit LDS wait per pair of activation fragments (fewer s_waitcnt in the MFMA stream)
 #endif
@@ -174,6 +177,12 @@ __device__ __forceinline__ void conv_lds(const char* __restrict__ ldsb, uint4* _
     const uint4* W = wsw + (size_t)(cw * NCO) * 64 + lane;
     // past the last k-step the refills read the next layer (or this layer's zero padding)
     const uint4* Wn = wnext ? wnext + (size_t)(cw * NCO) * 64 + lane : W + (size_t)KS * CF * 64;
+#if AZ_TOWER_BUFW
+    const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc((void*)wsw, (short)0, 0x7ffffff0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rN = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(wnext ? wnext : wsw + (size_t)KS * CF * 64), (short)0, 0x7ffffff0, 0x00020000);
+    const int voff = ((cw * NCO) * 64 + lane) * 16;
+#endif
     // B-fragment (activation) reads run LA fragments ahead, across k-step and tap boundaries:
     // the first LA reads of step s+1 are issued inside step s (not across a chunk-group
     // boundary, where the producers' flags are checked first).
@@ -250,12 +259,31 @@ __device__ __forceinline__ void conv_lds(const char* __restrict__ ldsb, uint4* _
                 else if (tap < 8) Wsrc = W + (size_t)((tap + 1) * NCH + half * CPH + c4 + PF - CPH) * CF * 64;
                 else if (half + 1 < NSPLIT) Wsrc = W + (size_t)((half + 1) * CPH + c4 + PF - CPH) * CF * 64;
                 else Wsrc = Wn + (size_t)(c4 + PF - CPH) * CF * 64;
+#if AZ_TOWER_BUFW
+                // buffer loads: SGPR descriptor + per-lane VGPR offset + the k-step's byte offset in an
+                // SGPR -- no 64-bit VALU address adds (and their carry-hazard nops) in the MFMA stream
+                {
+                    int kidx;
+                    bool nxt = false;
+                    if (c4 + PF < CPH) kidx = tap * NCH + cc + PF;
+                    else if (tap < 8) kidx = (tap + 1) * NCH + half * CPH + c4 + PF - CPH;
+                    else if (half + 1 < NSPLIT) kidx = (half + 1) * CPH + c4 + PF - CPH;
+                    else { kidx = c4 + PF - CPH; nxt = true; }
+                    const int soff = kidx * CF * 64 * 16;
+#pragma unroll
+                    for (int n = 0; n < NCO; n++)
+                        wr[c4 % PF][n] = __builtin_bit_cast(
+                            uint4, __builtin_amdgcn_raw_buffer_load_b128(nxt ? rN : rW, voff + n * 1024, soff, 0));
+                    (void)Wsrc;
+                }
+#else
 #pragma unroll
 #if defined(AZ_TOWER_L1W)   // experiment only: every k-step re-reads k-steps 0..1 (L1-resident weights)
                 for (int n = 0; n < NCO; n++) wr[c4 % PF][n] = W[(size_t)((c4 + PF) & 1) * CF * 64 + n * 64];
                 (void)Wsrc;
 #else
                 for (int n = 0; n < NCO; n++) wr[c4 % PF][n] = Wsrc[n * 64];
+#endif
 #endif
                 __builtin_amdgcn_sched_barrier(0);
                 const bool last_of_group = tap == 8 && c4 + 1 == CPH && half + 1 < NSPLIT;
