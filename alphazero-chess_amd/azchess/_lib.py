@@ -44,7 +44,8 @@ class AzEpisodeStep(C.Structure):
 class AzSearchStats(C.Structure):
     _fields_ = [("sims", C.c_int64), ("evals", C.c_int64), ("terminal_leaves", C.c_int64),
                 ("games_finished", C.c_int64), ("moves", C.c_int64), ("max_depth_sum", C.c_int64),
-                ("cache_hits", C.c_int64), ("cache_misses", C.c_int64)]
+                ("cache_hits", C.c_int64), ("cache_misses", C.c_int64), ("overflow", C.c_int64),
+                ("max_nodes", C.c_int64), ("max_edges", C.c_int64), ("node_cap", C.c_int64), ("edge_cap", C.c_int64)]
 
 
 class AzTiming(C.Structure):
@@ -94,6 +95,7 @@ SIGNATURES = [
     ("az_search_advance", C.c_int, [C.c_void_p, P(C.c_int32), C.c_int, P(C.c_int32)]),
     ("az_selfplay_reset", C.c_int, [C.c_void_p]),
     ("az_selfplay_step", C.c_int, [C.c_void_p, P(C.c_int), P(C.c_int)]),
+    ("az_selfplay_run_sims", C.c_int, [C.c_void_p, C.c_int, P(C.c_int), P(C.c_int), P(C.c_int)]),
     ("az_selfplay_drain", C.c_int, [C.c_void_p, P(AzEpisodeStep), C.c_int]),
     ("az_search_stats_get", C.c_int, [C.c_void_p, P(AzSearchStats)]),
     ("az_search_eval_log", C.c_int, [C.c_void_p, P(C.c_int64), P(C.c_int64), P(C.c_uint64), P(C.c_float),

@@ -71,7 +71,7 @@ def save_mpk(path, weights, blocks=NUM_RES_BLOCKS, filters=NUM_FILTERS):
     L.check(L.lib.az_net_save_mpk(str(path).encode(), int(blocks), int(filters), L.fptr(w), w.size))
 
 
-def load_model(path, blocks=NUM_RES_BLOCKS, filters=NUM_FILTERS, dtype="bf16", device=0):
+def load_model(path, blocks=NUM_RES_BLOCKS, filters=NUM_FILTERS, dtype="f32", device=0):
     """main.rs:109-116: AlphaZero::new().load_record(record)."""
     return AlphaZero(blocks, filters, weights=load_mpk(path, blocks, filters), dtype=dtype, device=device)
 
@@ -79,7 +79,7 @@ def load_model(path, blocks=NUM_RES_BLOCKS, filters=NUM_FILTERS, dtype="bf16", d
 class AlphaZero:
     """AlphaZero::new / forward (agent.rs:49-144) with weights resident in HBM."""
 
-    def __init__(self, blocks=NUM_RES_BLOCKS, filters=NUM_FILTERS, weights=None, dtype="bf16", device=0,
+    def __init__(self, blocks=NUM_RES_BLOCKS, filters=NUM_FILTERS, weights=None, dtype="f32", device=0,
                  seed=SEED):
         if weights is None:
             weights = random_weights(blocks, filters, seed)
@@ -90,8 +90,8 @@ class AlphaZero:
         h = C.c_void_p()
         L.check(L.lib.az_net_create(C.byref(desc), L.fptr(self.weights), self.weights.size, device, C.byref(h)))
         self._h = h
-        # libaz runs the fused tower kernel for bf16 nets unless AZ_FUSED_TOWER=0
-        self.fused_tower = dtype == "bf16" and os.environ.get("AZ_FUSED_TOWER", "1") != "0"
+        # libaz runs the fused tower kernel (f32 or bf16) unless AZ_FUSED_TOWER=0
+        self.fused_tower = os.environ.get("AZ_FUSED_TOWER", "1") != "0"
 
     def __del__(self):
         try:

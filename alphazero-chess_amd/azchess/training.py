@@ -58,6 +58,14 @@ class SelfPlay:
         L.check(L.lib.az_selfplay_step(self.search._h, C.byref(fin), C.byref(act)))
         return fin.value, act.value
 
+    def run_sims(self, nsims):
+        """The next `nsims` simulation steps of the current move of every game; when the move
+        completes, its action choice / play / re-root follow as in step().  Returns
+        (finished, active, move_done); active is -1 while the move is in progress."""
+        fin, act, done = C.c_int(), C.c_int(), C.c_int()
+        L.check(L.lib.az_selfplay_run_sims(self.search._h, int(nsims), C.byref(fin), C.byref(act), C.byref(done)))
+        return fin.value, act.value, bool(done.value)
+
     def drain(self):
         return [_convert(s) for s in self.drain_raw()]
 
@@ -202,15 +210,16 @@ class Trainer:
         L.check(L.lib.az_trainer_timing(self._h, C.byref(a), C.byref(b), C.byref(n), int(reset)))
         return a.value, b.value, n.value
 
-    def model(self, dtype="bf16"):
-        """model.valid() for self-play (training.rs:83): an inference net with the current weights."""
+    def model(self, dtype="f32"):
+        """model.valid() for self-play (training.rs:83): an inference net with the current weights,
+        f32 like the reference's Cuda<f32> backend (bf16 is an explicit throughput opt-in)."""
         from .agent import AlphaZero
         return AlphaZero(self.blocks, self.filters, weights=self.params(), dtype=dtype, device=self.device)
 
 
 def train(iterations, blocks=NUM_RES_BLOCKS, filters=NUM_FILTERS, games=NUM_EPISODES, sims=NUM_SIMULATIONS,
           min_replay=MIN_REPLAY_SIZE, train_steps=NUM_TRAIN_STEPS, batch_size=BATCH_SIZE, replay=None, trainer=None,
-          device=0, seed=SEED, dtype="bf16", comm=None, log=None):
+          device=0, seed=SEED, dtype="f32", comm=None, log=None):
     """train() (training.rs:39-275) without the TUI, arena and Elo (SKIP_VALIDATION = true,
     parameters.rs:35): per iteration, self-play `games` games with model.valid() until the replay
     buffer holds min_replay unique positions, then train_steps AdamW steps on batches of

@@ -111,8 +111,10 @@ struct NetDev {
     int blocks = 0, filters = 0, dtype = 0, device = 0;
     std::vector<void*> conv_w;      // swizzled MFMA fragments per conv (1 + 2*blocks)
     std::vector<float*> conv_b;     // folded bias per conv
+    std::vector<size_t> conv_bytes; // allocation size of each conv_w (incl. the 8 zero k-steps of prefetch pad)
     float* head = nullptr;          // folded head weights (f32)
     void* head_frag = nullptr;      // 1x1 F->40 head conv as bf16 hi/lo MFMA A-fragments (fused tower)
+    void* head_frag32 = nullptr;    // the same conv as f32 A-fragments of v_mfma_f32_16x16x4_f32 (f32 fused tower)
     size_t head_floats = 0;
     hipStream_t stream = nullptr;
     bool fused = true;              // use tower_forward when supported (AZ_FUSED_TOWER=0 disables)
@@ -163,7 +165,7 @@ int net_encode_rows(NetDev* n, const azc::Pos* npos, int NMAX, const int* row_ga
                     const int* count, int rows, void* planes, hipStream_t st);
 int synth_eval_rows(const int* count, int rows, const SearchOut& so, hipStream_t st);
 int net_planes_from_host_layout(NetDev* n, const float* d_in, int rows, void* planes, hipStream_t st);
-// fused tower (tower.hip): input conv + residual tower + heads in one launch, bf16 only.
+// fused tower (tower.hip): input conv + residual tower + heads in one launch (bf16 and f32).
 bool tower_supported(const NetDev* n);
 int tower_forward(NetDev* n, const void* planes, const int* count, int rows, float* pol, float* val,
                   const SearchOut* so, hipStream_t st);

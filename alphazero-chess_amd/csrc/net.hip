@@ -456,15 +456,19 @@ int net_create(const az_net_desc* d, const float* wts, size_t n, int device, Net
         const int CIN = cin == 19 ? 32 : cin;
         void* dw = nullptr;
         float* db = nullptr;
+        size_t bytes = 0;
         if (d->dtype == AZ_DTYPE_BF16) {
             auto s = swizzle_bf16(wf, F, cin, CIN);
-            if (hipMalloc(&dw, s.size() * 2) != hipSuccess) return -1;
-            if (hipMemcpy(dw, s.data(), s.size() * 2, hipMemcpyHostToDevice) != hipSuccess) return -1;
+            bytes = s.size() * 2;
+            if (hipMalloc(&dw, bytes) != hipSuccess) return -1;
+            if (hipMemcpy(dw, s.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) return -1;
         } else {
             auto s = swizzle_f32(wf, F, cin, CIN);
-            if (hipMalloc(&dw, s.size() * 4) != hipSuccess) return -1;
-            if (hipMemcpy(dw, s.data(), s.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return -1;
+            bytes = s.size() * 4;
+            if (hipMalloc(&dw, bytes) != hipSuccess) return -1;
+            if (hipMemcpy(dw, s.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) return -1;
         }
+        net->conv_bytes.push_back(bytes);
         if (hipMalloc(&db, F * 4) != hipSuccess) return -1;
         if (hipMemcpy(db, bf.data(), F * 4, hipMemcpyHostToDevice) != hipSuccess) return -1;
         net->conv_w.push_back(dw);
@@ -530,6 +534,18 @@ int net_create(const az_net_desc* d, const float* wts, size_t n, int device, Net
                     }
         AZ_HIP(hipMalloc(&net->head_frag, fr.size() * 2));
         AZ_HIP(hipMemcpy(net->head_frag, fr.data(), fr.size() * 2, hipMemcpyHostToDevice));
+        // f32 fused tower: the same 1x1 conv as exact f32 A-fragments of v_mfma_f32_16x16x4_f32,
+        // [kc F/16][cf 3][lane][4]: co = cf*16 + lane%16, ci = kc*16 + 4*(lane/16) + s
+        std::vector<float> f32fr((size_t)(F / 16) * 3 * 64 * 4, 0.0f);
+        for (int kc = 0; kc < F / 16; kc++)
+            for (int cf = 0; cf < 3; cf++)
+                for (int lane = 0; lane < 64; lane++)
+                    for (int s4 = 0; s4 < 4; s4++) {
+                        const int co = cf * 16 + (lane & 15), ci = kc * 16 + 4 * (lane >> 4) + s4;
+                        f32fr[(((size_t)kc * 3 + cf) * 64 + lane) * 4 + s4] = co < 40 ? hw[L.w40 + (size_t)co * F + ci] : 0.0f;
+                    }
+        AZ_HIP(hipMalloc(&net->head_frag32, f32fr.size() * 4));
+        AZ_HIP(hipMemcpy(net->head_frag32, f32fr.data(), f32fr.size() * 4, hipMemcpyHostToDevice));
     }
     *out = net;
     return 0;
@@ -542,6 +558,7 @@ void net_destroy(NetDev* n) {
     for (float* b : n->conv_b) (void)hipFree(b);
     (void)hipFree(n->head);
     (void)hipFree(n->head_frag);
+    (void)hipFree(n->head_frag32);
     (void)hipFree(n->x); (void)hipFree(n->h); (void)hipFree(n->planes);
     (void)hipFree(n->d_in); (void)hipFree(n->d_pol); (void)hipFree(n->d_val);
     if (n->stream) (void)hipStreamDestroy(n->stream);

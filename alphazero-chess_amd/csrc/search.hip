@@ -635,6 +635,7 @@ struct az_search {
     std::vector<az_episode_step> finished;
     size_t finished_read = 0;
     bool roots_fresh = false;        // trees sized for exactly S sims per root
+    int sim_cursor = 0;              // simulation steps of the current self-play move already run
     // timing
     bool timing = false;
     bool fused_steps = AZ_FUSED_STEPS != 0;   // k_step (backup + select + expand in one launch); env AZ_FUSED_STEPS=0: separate kernels
@@ -746,8 +747,10 @@ int eval_rows(az_search* s) {
     return synth_eval_rows(cnt, E.G, s->so, s->st);
 }
 
-int run_sims(az_search* s) {
+// simulation steps [i0, i1) of the current move (run_sims(s) = the whole move)
+int run_sims(az_search* s, int i0 = 0, int i1 = -1) {
     const int S = s->E.S;
+    if (i1 < 0) i1 = S;
     const bool tm = s->timing;
     if (tm && (int)s->ev.size() < EV_PER_STEP * S) {
         for (int i = (int)s->ev.size(); i < EV_PER_STEP * S; i++) {
@@ -760,7 +763,7 @@ int run_sims(az_search* s) {
     // costs a few us of GPU time: on every step it was ~20 % of a 6x64 simulation step); those
     // steps run as separate kernels, the others through the fused step kernel
     int pending = -1;                  // step whose backup is still to launch
-    for (int i = 0; i < S; i++) {
+    for (int i = i0; i < i1; i++) {
         const bool timed = tm && i % TIMING_EVERY == 0;
         int rc;
         if (timed || !s->fused_steps) {
@@ -779,12 +782,13 @@ int run_sims(az_search* s) {
         AZ_HIP(hipStreamSynchronize(s->st));
         std::vector<int> rows(S);
         AZ_HIP(hipMemcpy(rows.data(), s->E.batch_hist, S * 4, hipMemcpyDeviceToHost));
+        const int first_timed = (i0 + TIMING_EVERY - 1) / TIMING_EVERY * TIMING_EVERY;
         const bool net = s->cfg.evaluator == AZ_EVAL_NET;
         const double F = net ? s->net->dev->filters : 0.0;
         const double per_row_conv = 2.0 * 64.0 * 9.0 * F * F;
         const double per_row_tower = net ? net_tower_flop_per_eval(s->net->dev->blocks, s->net->dev->filters) : 0.0;
         const bool fused = net && s->net->dev->fused && tower_supported(s->net->dev);
-        for (int i = 0; i < S; i += TIMING_EVERY) {
+        for (int i = first_timed; i < i1; i += TIMING_EVERY) {
             hipEvent_t* e = &s->ev[EV_PER_STEP * i];
             float t[6], tc = 0.0f;
             for (int k = 0; k < 6; k++) (void)hipEventElapsedTime(&t[k], e[k], e[k + 1]);
@@ -1080,16 +1084,27 @@ int az_selfplay_reset(az_search* s) {
     s->pending.clear();
     s->finished.clear();
     s->finished_read = 0;
+    s->sim_cursor = 0;
     return setup_roots(s, s->cfg.noise, true);
 }
 
-int az_selfplay_step(az_search* s, int* finished, int* active) {
+static int selfplay_sims(az_search* s, int nsims, int* finished, int* active, int* move_done) {
     if (!s) return fail("null search");
+    if (nsims <= 0) return fail("az_selfplay_run_sims: nsims must be > 0");
     AZ_HIP(hipSetDevice(s->device));
     unsigned long long before = 0;
     AZ_HIP(hipMemcpy(&before, &s->E.ctr->games_finished, 8, hipMemcpyDeviceToHost));
-    int rc = run_sims(s);
+    const int i0 = s->sim_cursor, i1 = std::min(s->E.S, i0 + nsims);
+    int rc = run_sims(s, i0, i1);
     if (rc) return rc;
+    s->sim_cursor = i1;
+    if (move_done) *move_done = i1 == s->E.S;
+    if (i1 < s->E.S) {                 // the move is not complete: no action yet
+        if (finished) *finished = 0;
+        if (active) *active = -1;
+        return 0;
+    }
+    s->sim_cursor = 0;
     k_finish<<<s->E.G, 64, 0, s->st>>>(s->E, 0, nullptr, nullptr, s->cfg.noise);
     AZ_HIP(hipGetLastError());
     rc = drain_records(s);
@@ -1105,6 +1120,15 @@ int az_selfplay_step(az_search* s, int* finished, int* active) {
         *active = n;
     }
     return 0;
+}
+
+int az_selfplay_step(az_search* s, int* finished, int* active) {
+    if (s && s->sim_cursor != 0) return fail("az_selfplay_step: a move is in progress (az_selfplay_run_sims)");
+    return selfplay_sims(s, s ? s->E.S : 1, finished, active, nullptr);
+}
+
+int az_selfplay_run_sims(az_search* s, int nsims, int* finished, int* active, int* move_done) {
+    return selfplay_sims(s, nsims, finished, active, move_done);
 }
 
 int az_selfplay_drain(az_search* s, az_episode_step* out, int cap) {
@@ -1133,6 +1157,14 @@ int az_search_stats_get(az_search* s, az_search_stats* out) {
     out->max_depth_sum = (int64_t)c.depth_sum;
     out->cache_hits = (int64_t)c.cache_hits;
     out->cache_misses = (int64_t)c.evals;
+    out->overflow = c.overflow;
+    std::vector<int> nc(s->E.G), ec(s->E.G);
+    AZ_HIP(hipMemcpy(nc.data(), s->E.node_count, s->E.G * 4, hipMemcpyDeviceToHost));
+    AZ_HIP(hipMemcpy(ec.data(), s->E.edge_count, s->E.G * 4, hipMemcpyDeviceToHost));
+    out->max_nodes = *std::max_element(nc.begin(), nc.end());
+    out->max_edges = *std::max_element(ec.begin(), ec.end());
+    out->node_cap = s->E.NMAX;
+    out->edge_cap = s->E.EMAX;
     return 0;
 }
 

@@ -70,6 +70,8 @@ struct TowerArgs {
     const float* b[1 + 2 * 40];    // folded biases
     const float* head;
     const uint4* head_frag;        // 1x1 F->40 head conv as bf16 hi/lo MFMA A-fragments (net.hip)
+    const uint4* head_frag32;      // the same conv as f32 A-fragments (f32 tower)
+    unsigned wbytes[1 + 2 * 40];   // allocation bytes of each w[i] (buffer-load range check)
     int blocks;
 #ifdef AZ_TOWER_TRACE
     unsigned long long* trace;     // experiment only: [grid][TR_SLOTS] s_memrealtime stamps (100 MHz)
@@ -144,7 +146,8 @@ template <int CIN, int RSI, int F, int RSO, int BPW, int NCO, bool RESID, int NS
 __device__ __forceinline__ void conv_lds(const char* __restrict__ ldsb, uint4* __restrict__ out_lds, int in_off,
                                          int zero_off, const uint4* __restrict__ wsw, const uint4* __restrict__ wnext,
                                          const float* __restrict__ bias, uint4 (&wr)[RingPF<CIN / 32>::PF][NCO],
-                                         int cw, int bw, int lane, int wpar, unsigned long long* trw = nullptr,
+                                         int cw, int bw, int lane, int wpar, unsigned wbytes, unsigned nbytes,
+                                         unsigned long long* trw = nullptr,
                                          int* done = nullptr, int lidx = 0, int* prog = nullptr, int wid = 0,
                                          int partner = -1) {
     constexpr int NCH = CIN / 32;                     // 32-channel K chunks (4 slots)
@@ -178,9 +181,11 @@ __device__ __forceinline__ void conv_lds(const char* __restrict__ ldsb, uint4* _
     // past the last k-step the refills read the next layer (or this layer's zero padding)
     const uint4* Wn = wnext ? wnext + (size_t)(cw * NCO) * 64 + lane : W + (size_t)KS * CF * 64;
 #if AZ_TOWER_BUFW
-    const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc((void*)wsw, (short)0, 0x7ffffff0, 0x00020000);
+    // num_records = the real allocation (this layer's k-steps + its 8 zero k-steps of prefetch pad)
+    const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc((void*)wsw, (short)0, (int)wbytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rN = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(wnext ? wnext : wsw + (size_t)KS * CF * 64), (short)0, 0x7ffffff0, 0x00020000);
+        (void*)(wnext ? wnext : wsw + (size_t)KS * CF * 64), (short)0,
+        (int)(wnext ? nbytes : wbytes - (unsigned)KS * CF * 64 * 16), 0x00020000);
     const int voff = ((cw * NCO) * 64 + lane) * 16;
 #endif
     // B-fragment (activation) reads run LA fragments ahead, across k-step and tap boundaries:
@@ -376,11 +381,12 @@ __device__ __forceinline__ void conv_lds(const char* __restrict__ ldsb, uint4* _
     if (trw && lane == 0) trw[3] = __builtin_amdgcn_s_memtime();
 }
 
-// Heads v2 for NB boards [b0, b0 + NB) of the workgroup, from the LDS image x (bf16, row
-// stride RS slots), scratch in H; every one of the NT threads reaches every barrier.
+// Heads v2 for NB boards [b0, b0 + NB) of the workgroup, from the LDS image x (bf16, or f32 when
+// F32X, row stride RS slots), scratch in H; every one of the NT threads reaches every barrier.
 //   A: 1x1 F->40 (policy conv 32 + value conv 8, BN folded) on v_mfma_f32_16x16x32_bf16 with the
 //      f32 weights split into bf16 hi + lo fragments (16 mantissa bits; activations are bf16
-//      already), bias + ReLU -> p1v1 (f32);
+//      already), or for f32 activations on v_mfma_f32_16x16x4_f32 (exact f32), bias + ReLU ->
+//      p1v1 (f32);
 //   B: policy 1x1 32->64 on v_mfma_f32_16x16x4_f32 (exact f32 products) -> 4096 logits;
 //   C: value Linear 512->64 (K split over the waves), ReLU, Linear 64->1, tanh (f32 VALU);
 //   then softmax over 4096 and the dense rows or, in search mode, the priors gathered at the
@@ -393,7 +399,7 @@ template <int NB, int NT> struct HeadsScratch {
     static constexpr int FLOATS = STAT + NB * (2 * NW + 4);
 };
 
-template <int F, int RS, int NB, int NT, bool SEARCH>
+template <int F, int RS, int NB, int NT, bool SEARCH, bool F32X = false>
 __device__ __forceinline__ void heads_group(const char* __restrict__ xb, float* __restrict__ scr, int b0, int nb,
                                             int row0, int tid, const uint4* __restrict__ hfrag,
                                             const float* __restrict__ head, float* pol_out, float* val_out,
@@ -426,15 +432,32 @@ __device__ __forceinline__ void heads_group(const char* __restrict__ xb, float* 
         f32x4 acc[3];
 #pragma unroll
         for (int cf = 0; cf < 3; cf++) acc[cf] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        if constexpr (F32X) {
+            // f32 activations: exact f32 products on v_mfma_f32_16x16x4_f32, one 16-channel k-chunk
+            // (a float4 per lane) per 4 MFMAs
+#pragma unroll 4
+            for (int kc = 0; kc < F / 16; kc++) {
+                const f32x4 Bv = *reinterpret_cast<const f32x4*>(xr + kc * 64);
 #pragma unroll
-        for (int ks = 0; ks < F / 32; ks++) {
-            const bf16x8 Bv = *reinterpret_cast<const bf16x8*>(xr + ks * 64);
+                for (int cf = 0; cf < 3; cf++) {
+                    const f32x4 Av = __builtin_bit_cast(f32x4, hfrag[(kc * 3 + cf) * 64 + lane]);
 #pragma unroll
-            for (int cf = 0; cf < 3; cf++)
+                    for (int s4 = 0; s4 < 4; s4++)
+                        acc[cf] = __builtin_amdgcn_mfma_f32_16x16x4f32(Av[s4], Bv[s4], acc[cf], 0, 0, 0);
+                }
+            }
+        } else {
 #pragma unroll
-                for (int hl = 0; hl < 2; hl++)
-                    acc[cf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                        __builtin_bit_cast(bf16x8, hfrag[((ks * 3 + cf) * 2 + hl) * 64 + lane]), Bv, acc[cf], 0, 0, 0);
+            for (int ks = 0; ks < F / 32; ks++) {
+                const bf16x8 Bv = *reinterpret_cast<const bf16x8*>(xr + ks * 64);
+#pragma unroll
+                for (int cf = 0; cf < 3; cf++)
+#pragma unroll
+                    for (int hl = 0; hl < 2; hl++)
+                        acc[cf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                            __builtin_bit_cast(bf16x8, hfrag[((ks * 3 + cf) * 2 + hl) * 64 + lane]), Bv, acc[cf], 0, 0,
+                            0);
+            }
         }
 #pragma unroll
         for (int cf = 0; cf < 3; cf++)
@@ -670,24 +693,27 @@ tower_kernel(const __bf16* __restrict__ planes, TowerArgs ta, const int* __restr
         uint4 wr0[RingPF<1>::PF][NCO];
         ring_fill<1, F, NCO>(wr0, ta.w[0], cw, lane);
         conv_lds<32, RSI, F, RSF, BPW, NCO, false>(ldsb, X, XSZ * 16, zero_off, ta.w[0], nullptr, ta.b[0], wr0, cw,
-                                                   bw, lane, wpar);
+                                                   bw, lane, wpar, ta.wbytes[0], 0u);
     }
     TR_STAMP(2);
     uint4 wr[RingPF<F / 32>::PF][NCO];
     if (ta.blocks > 0) ring_fill<F / 32, F, NCO>(wr, ta.w[1], cw, lane);
     for (int b = 0; b < ta.blocks; b++) {
         const uint4* after = b + 1 < ta.blocks ? ta.w[3 + 2 * b] : nullptr;
+        const unsigned after_bytes = b + 1 < ta.blocks ? ta.wbytes[3 + 2 * b] : 0u;
 #ifdef AZ_TOWER_TRACE
         unsigned long long* trw = b == 10 ? ta.trace + (size_t)blockIdx.x * TR_SLOTS + 48 + w * 8 : nullptr;
 #else
         unsigned long long* trw = nullptr;
 #endif
         conv_lds<F, RSF, F, RSF, BPW, NCO, false, NSP>(ldsb, H, 0, zero_off, ta.w[1 + 2 * b], ta.w[2 + 2 * b],
-                                                       ta.b[1 + 2 * b], wr, cw, bw, lane, wpar, trw, done, 1 + 2 * b,
+                                                       ta.b[1 + 2 * b], wr, cw, bw, lane, wpar, ta.wbytes[1 + 2 * b],
+                                                       ta.wbytes[2 + 2 * b], trw, done, 1 + 2 * b,
                                                        prog, w, partner);
         conv_lds<F, RSF, F, RSF, BPW, NCO, true, NSP>(ldsb, X, XSZ * 16, zero_off, ta.w[2 + 2 * b], after,
-                                                      ta.b[2 + 2 * b], wr, cw, bw, lane, wpar,
-                                                      trw ? trw + 4 : nullptr, done, 2 + 2 * b, prog, w, partner);
+                                                      ta.b[2 + 2 * b], wr, cw, bw, lane, wpar, ta.wbytes[2 + 2 * b],
+                                                      after_bytes, trw ? trw + 4 : nullptr, done, 2 + 2 * b, prog, w,
+                                                      partner);
         TR_STAMP(3 + b);
     }
     if constexpr (NSP > 1) __syncthreads();           // the heads read every channel
@@ -712,8 +738,230 @@ tower_kernel(const __bf16* __restrict__ planes, TowerArgs ta, const int* __restr
 #endif
 }
 
+// ====================================================================== f32 tower
+// The reference evaluates in f32 (burn Cuda<f32>, main.rs:15,68; agent.rs:112-144).  This is the
+// same fused structure at that precision: activations f32 in LDS, weights f32, every product
+// an exact f32 FMA on v_mfma_f32_16x16x4_f32 (64 FLOP/clk/SIMD, the f32 peak, 157.3 TF).
+// At 1/16 of the bf16 rate a k-step is long (NCO*MF*4 MFMAs x 32 cycles per wave), so operand
+// delivery has ample slack: one board per workgroup (x and h f32 = 2 x 66 KB of LDS at F = 256),
+// B fragments double-buffered one k-step ahead, weight fragments two k-steps ahead.
+#ifndef AZ_T32_NCO256
+#define AZ_T32_NCO256 2    // F = 256: 16-channel output fragments per wave (2 = 8 waves, 2 per SIMD; 4 = 4 waves)
+#endif
+template <int F> struct Tower32Cfg;
+template <> struct Tower32Cfg<256> { static constexpr int BPB = 1, WB = 1, NCO = AZ_T32_NCO256; };
+template <> struct Tower32Cfg<128> { static constexpr int BPB = 1, WB = 1, NCO = 2; };
+template <> struct Tower32Cfg<64> { static constexpr int BPB = 1, WB = 1, NCO = 1; };
+template <> struct Tower32Cfg<32> { static constexpr int BPB = 2, WB = 2, NCO = 1; };
+constexpr int T32_PF = 2;  // weight k-steps in flight (register ring)
+
+// One f32 3x3 conv layer LDS -> LDS.  IN: CIN channels (16-channel k-chunks = 4 float4 slots),
+// row stride RSI slots; OUT: F channels, row stride RSO.  Wave (cw, bw) computes channels
+// [16*NCO*cw, +16*NCO) of boards [bw*BPW, +BPW).  A = weights (16 co x 4 ci), B = activations
+// (4 ci x 16 squares): one ds_read_b128 per lane holds 4 consecutive channels and feeds the 4
+// MFMAs of a k-chunk (k = 4h + s).  wr: weight ring, holds this layer's first T32_PF k-steps on
+// entry, the next layer's (rN) on exit.  The k-step byte offset rides in voffset, so the
+// descriptor's num_records bounds every refill.
+template <int CIN, int RSI, int F, int RSO, int BPW, int NCO, bool RESID>
+__device__ __forceinline__ void conv32_lds(const char* __restrict__ ldsb, char* __restrict__ outb, int in_off,
+                                           int zero_off, const __amdgpu_buffer_rsrc_t rW,
+                                           const __amdgpu_buffer_rsrc_t rN, const float* __restrict__ bias,
+                                           f32x4 (&wr)[T32_PF][NCO], int cw, int bw, int lane) {
+    constexpr int NCH = CIN / 16;
+    constexpr int CF = F / 16;
+    constexpr int MF = BPW * 4;
+    constexpr int PF = T32_PF;
+    constexpr int KB = CF * 64 * 16;                  // bytes per k-step (all output fragments)
+    static_assert(NCH % PF == 0, "ring slots must be compile-time");
+    const int h = lane >> 4, l16 = lane & 15;
+    f32x4 acc[MF][NCO];
+#pragma unroll
+    for (int n = 0; n < NCO; n++) {
+        const float4 bn = *reinterpret_cast<const float4*>(bias + cw * 16 * NCO + n * 16 + h * 4);
+#pragma unroll
+        for (int m = 0; m < MF; m++) acc[m][n] = f32x4{bn.x, bn.y, bn.z, bn.w};
+    }
+    const int voff = ((cw * NCO) * 64 + lane) * 16;
+    // per-tap B addresses, branch-free: off-board taps read the zero row at the same slot mod 16
+    const int lane_off = ((l16 * RSI) + h) * 16;
+    const int lr = l16 >> 3, lf = l16 & 7;
+    auto tap_bases = [&](int tap, int* base) {
+        const int dr = tap / 3 - 1, df = tap % 3 - 1;
+        const bool okf = (unsigned)(lf + df) < 8u;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const bool ok = okf && (unsigned)(2 * q + lr + dr) < 8u;
+#pragma unroll
+            for (int bb = 0; bb < BPW; bb++) {
+                const int m = bb * 4 + q;
+                const int va = lane_off + (((bw * BPW + bb) * 64 + q * 16 + dr * 8 + df) * RSI) * 16 + in_off;
+                base[m] = ok ? va : ((va & 0xF0) | zero_off);
+            }
+        }
+    };
+    int bcur[MF], bnx[MF];
+    f32x4 bq[MF], bn[MF];
+    tap_bases(0, bcur);
+#pragma unroll
+    for (int m = 0; m < MF; m++) bq[m] = *reinterpret_cast<const f32x4*>(ldsb + bcur[m]);
+#pragma unroll 1
+    for (int tap = 0; tap < 9; tap++) {
+        tap_bases(tap < 8 ? tap + 1 : 8, bnx);
+#pragma unroll
+        for (int c = 0; c < NCH; c++) {
+            // next k-step's B fragments (same tap, next chunk; or the next tap's first chunk) and the
+            // weight refill are issued first: a whole k-step of MFMAs covers their latency
+#pragma unroll
+            for (int m = 0; m < MF; m++)
+                bn[m] = *reinterpret_cast<const f32x4*>(ldsb + (c + 1 < NCH ? bcur[m] + (c + 1) * 64 : bnx[m]));
+            f32x4 a[NCO];
+#pragma unroll
+            for (int n = 0; n < NCO; n++) a[n] = wr[c % PF][n];
+            // refill the slot with the k-step PF later: this tap, the next tap, or the next layer
+            {
+                int kidx;
+                bool nxt = false;
+                if (c + PF < NCH) kidx = tap * NCH + c + PF;
+                else if (tap < 8) kidx = (tap + 1) * NCH + c + PF - NCH;
+                else { kidx = c + PF - NCH; nxt = true; }
+#pragma unroll
+                for (int n = 0; n < NCO; n++)
+                    wr[c % PF][n] = __builtin_bit_cast(
+                        f32x4, __builtin_amdgcn_raw_buffer_load_b128(nxt ? rN : rW, voff + n * 1024 + kidx * KB, 0, 0));
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int s4 = 0; s4 < 4; s4++)
+#pragma unroll
+                for (int m = 0; m < MF; m++)
+#pragma unroll
+                    for (int n = 0; n < NCO; n++)
+                        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[n][s4], bq[m][s4], acc[m][n], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int m = 0; m < MF; m++) bq[m] = bn[m];
+        }
+#pragma unroll
+        for (int m = 0; m < MF; m++) bcur[m] = bnx[m];
+    }
+    // epilogue: (+ residual) + ReLU, 4 consecutive channels of one square per lane (16-B stores);
+    // `in` and `out` are different buffers, the barrier after publishes `out`
+#pragma unroll
+    for (int n = 0; n < NCO; n++) {
+        const int co = cw * 16 * NCO + n * 16 + h * 4;
+        char* lane_base = outb + ((bw * BPW * 64 + l16) * RSO + (co >> 2)) * 16;
+#pragma unroll
+        for (int m = 0; m < MF; m++) {
+            f32x4* dst = reinterpret_cast<f32x4*>(lane_base + ((m >> 2) * 64 + (m & 3) * 16) * RSO * 16);
+            f32x4 v = acc[m][n];
+            if constexpr (RESID) v += *dst;
+#pragma unroll
+            for (int r = 0; r < 4; r++) v[r] = fmaxf(v[r], 0.0f);
+            *dst = v;
+        }
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t t32_rsrc(const uint4* p, unsigned bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, 0x00020000);
+}
+
+template <int F, bool SEARCH>
+__global__ void __launch_bounds__((F / (16 * Tower32Cfg<F>::NCO)) * Tower32Cfg<F>::WB * 64)
+tower32_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __restrict__ count_ptr, int rows,
+               float* __restrict__ pol_out, float* __restrict__ val_out, SearchOut so) {
+    constexpr int BPB = Tower32Cfg<F>::BPB, WB = Tower32Cfg<F>::WB, BPW = BPB / WB, NCO = Tower32Cfg<F>::NCO;
+    constexpr int NCW = F / (16 * NCO);
+    constexpr int NT = NCW * WB * 64;
+    constexpr int RSF = F / 4 + 2, RSI = 32 / 4 + 2;  // f32 rows: F/4 slots + 2 pad (conflict-free b128 reads)
+    constexpr int XSZ = BPB * 64 * RSF;
+    constexpr int ZN = 16 + F / 4;
+    constexpr int NBH = HeadsCfg<F>::NB < BPB ? HeadsCfg<F>::NB : BPB;
+    constexpr int HSZ0 = (HeadsScratch<NBH, NT>::FLOATS * 4 + 15) / 16;
+    constexpr int HSZ = ((XSZ > HSZ0 ? XSZ : HSZ0) + 15) / 16 * 16;
+    static_assert(BPB * 64 * RSI <= HSZ, "input planes must fit in h");
+    __shared__ __attribute__((aligned(16))) uint4 lds[XSZ + HSZ + ZN];
+    const int count = count_ptr ? min(*count_ptr, rows) : rows;
+    const int row0 = blockIdx.x * BPB;
+    if (row0 >= count) return;
+    const int nb = min(BPB, count - row0);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int cw = w % NCW, bw = w / NCW;
+    uint4* X = lds;
+    uint4* H = lds + XSZ;
+    const int zero_off = (XSZ + HSZ) * 16;
+    const char* ldsb = reinterpret_cast<const char*>(lds);
+
+    // input planes [row][64][32] f32 -> H, row stride RSI
+    if (planes) {
+        const uint4* src = reinterpret_cast<const uint4*>(planes) + (size_t)row0 * 64 * 8;
+        for (int c = tid; c < BPB * 64 * 8; c += NT) {
+            const int rowi = c >> 3, slot = c & 7;
+            H[rowi * RSI + slot] = rowi < nb * 64 ? src[c] : make_uint4(0, 0, 0, 0);
+        }
+    } else {
+        // search mode: to_tensor (chess.rs:191-245) from the leaf's packed position, one thread per square
+        for (int rowi = tid; rowi < BPB * 64; rowi += NT) {
+            float v[32];
+#pragma unroll
+            for (int c = 0; c < 32; c++) v[c] = 0.0f;
+            if (rowi < nb * 64) {
+                const int row = row0 + (rowi >> 6), sq = rowi & 63;
+                const azc::Pos p = so.npos[(size_t)so.row_game[row] * so.NMAX + so.row_node[row]];
+#pragma unroll
+                for (int c = 0; c < 19; c++) v[c] = azc::plane_value(p, c, sq);
+            }
+            uint4 q[8];
+            __builtin_memcpy(q, v, sizeof(v));
+#pragma unroll
+            for (int k = 0; k < 8; k++) H[rowi * RSI + k] = q[k];
+        }
+    }
+    for (int c = tid; c < ZN; c += NT) lds[XSZ + HSZ + c] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+
+    f32x4 wr[T32_PF][NCO];
+    {
+        const __amdgpu_buffer_rsrc_t r0 = t32_rsrc(ta.w[0], ta.wbytes[0]);
+        const __amdgpu_buffer_rsrc_t r1 =
+            ta.blocks > 0 ? t32_rsrc(ta.w[1], ta.wbytes[1]) : t32_rsrc(ta.w[0] + 18 * (F / 16) * 64, ta.wbytes[0] - 18 * (F / 16) * 1024);
+        const int voff = ((cw * NCO) * 64 + lane) * 16;
+#pragma unroll
+        for (int i = 0; i < T32_PF; i++)
+#pragma unroll
+            for (int n = 0; n < NCO; n++)
+                wr[i][n] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                         r0, voff + n * 1024 + i * (F / 16) * 1024, 0, 0));
+        conv32_lds<32, RSI, F, RSF, BPW, NCO, false>(ldsb, reinterpret_cast<char*>(X), XSZ * 16, zero_off, r0, r1,
+                                                     ta.b[0], wr, cw, bw, lane);
+    }
+    for (int b = 0; b < ta.blocks; b++) {
+        const int i1 = 1 + 2 * b, i2 = 2 + 2 * b;
+        const __amdgpu_buffer_rsrc_t r1 = t32_rsrc(ta.w[i1], ta.wbytes[i1]);
+        const __amdgpu_buffer_rsrc_t r2 = t32_rsrc(ta.w[i2], ta.wbytes[i2]);
+        // after the block's second conv the ring prefetches the next block's first conv (or
+        // reads this conv's zero pad after the last one)
+        const __amdgpu_buffer_rsrc_t r3 =
+            b + 1 < ta.blocks ? t32_rsrc(ta.w[i2 + 1], ta.wbytes[i2 + 1])
+                              : t32_rsrc(ta.w[i2] + (size_t)9 * (F / 16) * (F / 16) * 64,
+                                         ta.wbytes[i2] - 9u * (F / 16) * (F / 16) * 1024);
+        conv32_lds<F, RSF, F, RSF, BPW, NCO, false>(ldsb, reinterpret_cast<char*>(H), 0, zero_off, r1, r2,
+                                                    ta.b[i1], wr, cw, bw, lane);
+        conv32_lds<F, RSF, F, RSF, BPW, NCO, true>(ldsb, reinterpret_cast<char*>(X), XSZ * 16, zero_off, r2, r3,
+                                                   ta.b[i2], wr, cw, bw, lane);
+    }
+    static_assert(HeadsScratch<NBH, NT>::FLOATS * 4 <= HSZ * 16, "heads scratch must fit in h");
+    static_assert((16 * NBH) % (NT / 64) == 0, "policy tiles must divide over the waves");
+    for (int b0 = 0; b0 < BPB && b0 < nb; b0 += NBH)
+        heads_group<F, RSF, NBH, NT, SEARCH, true>(ldsb, reinterpret_cast<float*>(H), b0, nb, row0, tid,
+                                                   ta.head_frag32, ta.head, pol_out, val_out, so, nullptr);
+}
+
+
 bool tower_supported(const NetDev* n) {
-    return n->dtype == AZ_DTYPE_BF16 && n->blocks <= 40 &&
+    return (n->dtype == AZ_DTYPE_BF16 || n->dtype == AZ_DTYPE_F32) && n->blocks <= 40 &&
            (n->filters == 256 || n->filters == 128 || n->filters == 64 || n->filters == 32);
 }
 
@@ -731,6 +979,8 @@ int tower_forward(NetDev* n, const void* planes, const int* count, int rows, flo
     }
     ta.head = n->head;
     ta.head_frag = reinterpret_cast<const uint4*>(n->head_frag);
+    ta.head_frag32 = reinterpret_cast<const uint4*>(n->head_frag32);
+    for (int i = 0; i < 1 + 2 * n->blocks; i++) ta.wbytes[i] = (unsigned)n->conv_bytes[i];
     ta.blocks = n->blocks;
 #ifdef AZ_TOWER_TRACE
     // experiment only: stamp launch number AZ_TOWER_TRACE of this process into $AZ_TOWER_TRACE_FILE
@@ -767,8 +1017,22 @@ int tower_forward(NetDev* n, const void* planes, const int* count, int rows, flo
         TRACE_DUMP(grid);                                                                                      \
         return hipGetLastError() == hipSuccess ? 0 : fail("tower launch failed");                              \
     }
+#define AZ_TOWER32(FF)                                                                                          \
+    if (n->filters == FF) {                                                                                    \
+        constexpr int BPB = Tower32Cfg<FF>::BPB;                                                               \
+        constexpr int NT = (FF / (16 * Tower32Cfg<FF>::NCO)) * Tower32Cfg<FF>::WB * 64;                        \
+        const int grid = (rows + BPB - 1) / BPB;                                                               \
+        if (so) tower32_kernel<FF, true><<<grid, NT, 0, st>>>((const float*)planes, ta, count, rows, pol, val, s); \
+        else tower32_kernel<FF, false><<<grid, NT, 0, st>>>((const float*)planes, ta, count, rows, pol, val, s);  \
+        return hipGetLastError() == hipSuccess ? 0 : fail("f32 tower launch failed");                          \
+    }
+    if (n->dtype == AZ_DTYPE_F32) {
+        AZ_TOWER32(256) AZ_TOWER32(128) AZ_TOWER32(64) AZ_TOWER32(32)
+        return fail("fused tower: unsupported filters");
+    }
     AZ_TOWER(256) AZ_TOWER(128) AZ_TOWER(64) AZ_TOWER(32)
 #undef AZ_TOWER
+#undef AZ_TOWER32
     return fail("fused tower: unsupported filters");
 }
 

@@ -2,21 +2,26 @@
 
 Workload (BASELINE.json configs[2], "C3"): 2048 concurrent self-play games per GPU,
 800 simulations per move, 20-block x 256-filter AlphaZero net (agent.rs), random-init
-weights (seed 42), all games from the start position (training.rs:344-358).
-One "step" = one move of every game = games x 800 simulations (select, expand, batched
-network evaluation, backup) + action choice / play / re-root.  Games that end are
-restarted in their slot, so every step does exactly games x sims simulations.
-Multi-GPU: one process per GPU, games sharded (different seeds), no collective on the
-path; barrier + max-over-ranks timing only.
+weights (seed 42), all games from the start position (training.rs:344-358), evaluated in
+f32 like the reference (burn Cuda<f32>, main.rs:15,68).
+One "step" = `--sims-per-step` (default 100) simulation steps of every game, i.e. games x 100
+simulations (select, expand, batched network evaluation, backup); every 8th step completes a
+move (800 sims), whose action choice / play / re-root fall inside that step.  Games that end
+are restarted in their slot, so every step does exactly games x sims-per-step simulations.
+Multi-GPU: one process per GPU (torchrun, or `--gpus N` spawns the N ranks itself), games
+sharded (different seeds), no collective on the path; barrier + max-over-ranks timing only.
 
-Extra JSON fields: roofline (the residual 3x3 conv kernel vs bf16 dense MFMA peak,
-measured with HIP events on the engine stream over the timed region), tree_walk (select
-kernel, algorithmic bytes / time vs HBM peak), cpu_baseline (the oracle, rank 0, N=1,
-bounded sample).
+Extra JSON fields: roofline (the fused tower kernel vs the f32 MFMA peak, HIP events on the
+engine stream over the timed region), bf16_mode (the same window with the bf16 tower, labelled,
+with its stated tolerance), tree_walk (select kernel, algorithmic bytes / time vs HBM peak),
+cpu_baseline (the oracle, rank 0, N=1, bounded sample), training (the C5 gradient step).
+`--rehearse` runs the multi-rank plumbing with a CPU stub engine (no GPU; CI only).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -27,21 +32,27 @@ PEAK_BF16_TFLOPS = 2500.0     # MI355X_MICROARCH.md: ~2.5 PF dense bf16
 PEAK_F32_TFLOPS = 157.3       # MI355X_MICROARCH.md: f32 MFMA = vector peak
 PEAK_HBM_GBS = 8000.0         # MI355X_MICROARCH.md: 8.0 TB/s spec
 # HBM bytes per tower launch from rocprofv3 PMC passes (tools/pmc_run.sh: FETCH_SIZE x2 per the
-# gfx950 correction + WRITE_SIZE), same kernel and per-launch work (2048 rows, 20x256 bf16)
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_tower_v11_summary.json")
+# gfx950 correction + WRITE_SIZE), same kernel and per-launch work (2048 rows, 20x256)
+PMC_SUMMARY = {"f32": os.path.join(ROOT, "profiles", "r02_pmc_tower32_summary.json"),
+               "bf16": os.path.join(ROOT, "profiles", "r01_pmc_tower_v11_summary.json")}
 # mean plies of complete self-play games of this config (tools/game_length.py: 256 games, 20x256
 # random-init seed 42, 800 sims/move, noise + temperature moves, played to the end)
 GAME_LENGTH = os.path.join(ROOT, "profiles", "r01_game_length_256.json")
+# stated tolerances of the two tower precisions against the f32 oracle (tests/test_gpu_net.py)
+TOLERANCE = {"f32": "value |d| <= 1e-5, policy |d| <= 1e-4 p + 1e-8 (tests/test_gpu_net.py)",
+             "bf16": "value |d| <= 2e-2, policy |d| <= 5e-2 p + 2e-5, total variation <= 2e-2 "
+                     "(tests/test_gpu_net.py)"}
 
 
 def pmc_traffic(games, blocks, filters, dtype):
     """Per-launch HBM traffic of the dominant kernel from the committed PMC summary, or None
     when the bench workload is not the one the counters were collected on."""
-    if (games, blocks, filters, dtype) != (2048, 20, 256, "bf16") or not os.path.exists(PMC_SUMMARY):
+    path = PMC_SUMMARY.get(dtype)
+    if (games, blocks, filters) != (2048, 20, 256) or not path or not os.path.exists(path):
         return None, None
-    with open(PMC_SUMMARY) as f:
+    with open(path) as f:
         s = json.load(f)
-    return s.get("traffic_bytes"), os.path.relpath(PMC_SUMMARY, ROOT)
+    return s.get("traffic_bytes"), os.path.relpath(path, ROOT)
 
 
 def cpu_baseline(blocks, filters, threads, games, sims):
@@ -102,7 +113,6 @@ def train_child(a):
 def train_phase(args, A, rank, world, local):
     """Run train_child on every rank (subprocess with a time limit, so a collective that never
     completes cannot hold the self-play measurement hostage); rank 0 returns the summary."""
-    import subprocess
     uid = ""
     if world > 1:
         import torch.distributed as dist
@@ -163,17 +173,96 @@ def config_name(games, sims, blocks, filters):
     return "custom (not a BASELINE.json config)"
 
 
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` without a torchrun environment: start N fresh child processes of this
+    script, one per GPU (RANK = LOCAL_RANK = i, WORLD_SIZE = N, rendezvous on 127.0.0.1), and exit
+    with the worst child status.  Runs before anything touches the GPU (no exec: children)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+class _RehearsalSearch:
+    """Counters / timing of the CPU stub engine (same keys as BatchedSearch)."""
+
+    def __init__(self, games):
+        self.games = games
+        self.c = dict(sims=0, evals=0, terminal_leaves=0, moves=0, max_depth_sum=0, cache_hits=0)
+
+    def stats(self):
+        return dict(self.c)
+
+    def timing(self, reset=False, enable=None):
+        keys = ("select", "expand", "encode", "tower", "heads", "backup", "conv")
+        t = {k + "_ms": 0.0 for k in keys}
+        t.update(conv_flop=0.0, tower_flop=0.0, conv_launches=0, select_launches=0, sim_steps=0, select_bytes=0.0)
+        return t
+
+
+class RehearsalSelfPlay:
+    """`--rehearse`: a CPU stand-in for azchess.SelfPlay with the same interface, so the multi-rank
+    plumbing of bench.py (spawn, per-rank seeds, barrier, max-over-ranks, counter sums, JSON line)
+    runs in a container without a GPU.  It does a little numpy work per simulation step; its
+    numbers measure nothing and are labelled as such."""
+
+    def __init__(self, games, sims, seed):
+        import numpy as np
+        self.np, self.games, self.S = np, games, sims
+        self.rng = np.random.default_rng(seed)
+        self.search = _RehearsalSearch(games)
+        self.cursor = 0
+
+    def reset(self):
+        self.cursor = 0
+
+    def run_sims(self, n):
+        n = min(n, self.S - self.cursor)
+        a = self.rng.standard_normal((64, 64)).astype(self.np.float32)
+        for _ in range(n):
+            a = self.np.tanh(a @ a.T * 1e-2)
+        self.cursor += n
+        self.search.c["sims"] += self.games * n
+        self.search.c["evals"] += self.games * n
+        done = self.cursor == self.S
+        if done:
+            self.cursor = 0
+            self.search.c["moves"] += self.games
+        return 0, (self.games if done else -1), done
+
+    def drain(self):
+        return []
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--games", type=int, default=2048)
     ap.add_argument("--sims", type=int, default=800)
+    ap.add_argument("--sims-per-step", type=int, default=100, help="simulation steps of every game per bench step")
     ap.add_argument("--blocks", type=int, default=20)
     ap.add_argument("--filters", type=int, default=256)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
-    ap.add_argument("--cache", type=int, default=500000, help="FEN cache entries (CACHE_CAPACITY, 0 = off)")
+    ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"],
+                    help="headline precision (the reference computes in f32)")
+    ap.add_argument("--bf16-steps", type=int, default=-1,
+                    help="steps of the labelled bf16_mode leg (-1 = same as --steps, 0 = skip)")
+    ap.add_argument("--cache", type=int, default=0,
+                    help="FEN cache entries for an extra with_fen_cache leg (CACHE_CAPACITY = 500000; 0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-games", type=int, default=16)
@@ -181,6 +270,8 @@ def main():
     ap.add_argument("--train-steps", type=int, default=5, help="timed training steps (0 = skip the training phase)")
     ap.add_argument("--train-batch", type=int, default=512, help="positions per rank (BATCH_SIZE, parameters.rs:17)")
     ap.add_argument("--train-timeout", type=int, default=240)
+    ap.add_argument("--rehearse", action="store_true",
+                    help="no GPU: run the rank plumbing with a CPU stub engine (gloo); numbers are meaningless")
     ap.add_argument("--train-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--rank", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--world", type=int, default=1, help=argparse.SUPPRESS)
@@ -189,40 +280,58 @@ def main():
     args = ap.parse_args()
     if args.train_child:
         return train_child(args)
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args.gpus)
 
-    # libaz (and the /opt/rocm HIP runtime it is built for) is loaded before torch: torch
-    # bundles its own libamdhip64.so.7 (same SONAME) and is only used here for the gloo
-    # barrier / reduction between ranks -- the self-play path has no collective.
-    import azchess as A
     from azchess.dist import barrier as dist_barrier, env_rank, reduce_run, shard
     rank, world, local = env_rank()
-    import ctypes
-    ndev = ctypes.c_int(0)
-    A._lib.lib.az_device_count(ctypes.byref(ndev))
-    if ndev.value < 1:
-        raise SystemExit("bench.py: no GPU visible to libaz")
-    local = local % ndev.value          # one GPU per rank; wraps only when rehearsing on fewer GPUs
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    G, S, K = args.games, args.sims, args.sims_per_step
+    if K < 1 or S % K:
+        raise SystemExit("bench.py: --sims-per-step must divide --sims")
+
+    if args.rehearse:
+        A = None
+        ndev = world
+
+        def synchronize():
+            pass
+    else:
+        # libaz (and the /opt/rocm HIP runtime it is built for) is loaded before torch: torch
+        # bundles its own libamdhip64.so.7 (same SONAME) and is only used here for the gloo
+        # barrier / reduction between ranks -- the self-play path has no collective.
+        import ctypes
+        import azchess as A
+        n = ctypes.c_int(0)
+        A._lib.lib.az_device_count(ctypes.byref(n))
+        ndev = n.value
+
+        def synchronize():
+            A._lib.check(A._lib.lib.az_device_synchronize(local))
+    if ndev < world or local >= ndev:
+        raise SystemExit("bench.py: %d ranks need %d GPUs, %d visible" % (world, world, ndev))
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")
-
-    G, S = args.games, args.sims
-    net = A.AlphaZero(args.blocks, args.filters, dtype=args.dtype, device=local, seed=42)
     sh = shard(rank, world, G)
-
-    def synchronize():
-        A._lib.check(A._lib.lib.az_device_synchronize(local))
 
     def barrier():
         dist_barrier(world)
         synchronize()
 
-    def phase(cache, steps, timing):
-        """Self-play from startpos: warmup moves, then `steps` timed moves of every game."""
-        sp = A.SelfPlay(net, games=G, sims=S, device=local, continuous=True, seed=sh["seed"], cache_capacity=cache)
+    def phase(net, cache, steps, timing):
+        """Self-play from startpos: warmup steps, then `steps` timed steps of K simulation steps."""
+        if args.rehearse:
+            sp = RehearsalSelfPlay(G, S, sh["seed"])
+        else:
+            sp = A.SelfPlay(net, games=G, sims=S, device=local, continuous=True, seed=sh["seed"],
+                            cache_capacity=cache)
         sp.reset()
         for _ in range(args.warmup):
-            sp.step()
+            sp.run_sims(K)
             sp.drain()
         st0 = sp.search.stats()
         sp.search.timing(reset=True, enable=timing)
@@ -230,7 +339,7 @@ def main():
         t0 = time.perf_counter()
         finished = 0
         for _ in range(steps):
-            f, _ = sp.step()
+            f, _, _ = sp.run_sims(K)
             finished += f
             sp.drain()
         synchronize()
@@ -239,36 +348,79 @@ def main():
         tm = sp.search.timing(reset=False, enable=False)
         st1 = sp.search.stats()
         c = [st1[k] - st0[k] for k in ("sims", "evals", "terminal_leaves", "moves", "max_depth_sum", "cache_hits")]
-        assert c[0] == G * S * steps, (c[0], G * S * steps)
+        assert c[0] == G * K * steps, (c[0], G * K * steps)
         elapsed, tot = reduce_run(elapsed, c + [finished], world)
         del sp
         return elapsed, dict(zip(("sims", "evals", "terminal", "moves", "depth", "hits", "finished"), tot)), tm, c[0]
 
-    # headline: no FEN cache -> every non-terminal simulation evaluates its leaf on the network
-    elapsed, tot, tm, sims_rank = phase(0, args.steps, True)
+    def roofline(tm, dtype, fused):
+        peak = PEAK_BF16_TFLOPS if dtype == "bf16" else PEAK_F32_TFLOPS
+        conv_tflops = tm["conv_flop"] / (tm["conv_ms"] * 1e-3) / 1e12 if tm["conv_ms"] > 0 else 0.0
+        traffic, traffic_src = pmc_traffic(G, args.blocks, args.filters, dtype)
+        kname = "tower_kernel" if dtype == "bf16" else "tower32_kernel"
+        return {"bound": "mfma", "achieved": conv_tflops, "peak": peak, "unit": "TFLOP/s",
+                "frac": conv_tflops / peak, "traffic": traffic,
+                "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
+                "kernel": ("%s<%d> (fused input conv + %d residual convs + heads, %s; algorithmic FLOPs = conv "
+                           "FLOPs only), %d launches timed (HIP events on every 8th simulation step)"
+                           % (kname, args.filters, 2 * args.blocks,
+                              "v_mfma_f32_16x16x32_bf16" if dtype == "bf16" else "v_mfma_f32_16x16x4_f32",
+                              tm["conv_launches"]))
+                          if fused else
+                          "conv3x3_kernel<%d,%d> (residual 3x3 conv), %d launches timed" %
+                          (args.filters, args.filters, tm["conv_launches"]),
+                "flop_per_launch": tm["conv_flop"] / max(tm["conv_launches"], 1),
+                "avg_ms_per_launch": tm["conv_ms"] / max(tm["conv_launches"], 1)}
+
+    def make_net(dtype):
+        if args.rehearse:
+            return None
+        return A.AlphaZero(args.blocks, args.filters, dtype=dtype, device=local, seed=42)
+
+    # headline: reference precision, no FEN cache -> every non-terminal simulation evaluates its
+    # leaf on the network
+    net = make_net(args.dtype)
+    elapsed, tot, tm, sims_rank = phase(net, 0, args.steps, True)
+    fused = net.fused_tower if net is not None else False
+    del net
     sims_all, evals_all, term_all = tot["sims"], tot["evals"], tot["terminal"]
     fin_all, moves_all, depth_all = tot["finished"], tot["moves"], tot["depth"]
-    # the reference's FEN cache (tree.rs:214-219, CACHE_CAPACITY = 500k) on the same window
+
+    # the bf16 throughput mode beside it (labelled; not the headline)
+    bf16_res = None
+    bf16_steps = args.steps if args.bf16_steps < 0 else args.bf16_steps
+    if args.dtype == "f32" and bf16_steps > 0:
+        net16 = make_net("bf16")
+        e16, t16, tm16, _ = phase(net16, 0, bf16_steps, True)
+        bf16_res = {"value": t16["sims"] / e16, "unit": "sims/s", "steps": bf16_steps,
+                    "ms_per_step": e16 / bf16_steps * 1e3, "dtype": "bf16",
+                    "roofline": roofline(tm16, "bf16", net16.fused_tower if net16 is not None else False),
+                    "tolerance_vs_f32_oracle": TOLERANCE["bf16"],
+                    "note": "bf16 weights/activations, f32 accumulate: narrower than the reference's f32, "
+                            "reported beside the headline, not as it"}
+        del net16
+
+    # the reference's FEN cache (tree.rs:214-219) on the same window, on request
     cache_res = None
     if args.cache > 0:
-        e2, t2, _, _ = phase(args.cache, args.steps, False)
+        netc = make_net(args.dtype)
+        e2, t2, _, _ = phase(netc, args.cache, args.steps, False)
         cache_res = {"value": t2["sims"] / e2, "unit": "sims/s", "evals_per_sim": t2["evals"] / max(t2["sims"], 1),
-                     "cache_hit_frac": t2["hits"] / max(t2["sims"], 1), "entries": args.cache,
-                     "note": "same window with the reference's FEN evaluation cache (A12); games are in "
-                             "lockstep from startpos, so early moves share most positions"}
+                     "cache_hit_frac": t2["hits"] / max(t2["sims"], 1), "entries": args.cache}
+        del netc
 
-    training = train_phase(args, A, rank, world, local) if args.train_steps > 0 else None
+    training = None
+    if args.train_steps > 0 and not args.rehearse:
+        training = train_phase(args, A, rank, world, local)
     if rank != 0:
         dist.destroy_process_group()
         return
     value = sims_all / elapsed
-    traffic, traffic_src = pmc_traffic(G, args.blocks, args.filters, args.dtype)
-    peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
-    conv_tflops = tm["conv_flop"] / (tm["conv_ms"] * 1e-3) / 1e12 if tm["conv_ms"] > 0 else 0.0
     tower_tflops = tm["tower_flop"] / (tm["tower_ms"] * 1e-3) / 1e12 if tm["tower_ms"] > 0 else 0.0
-    # select_bytes covers every k_select launch of the window (steps x S); the event times cover
+    peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
+    # select_bytes covers every k_select launch of the window (steps x K); the event times cover
     # the sampled launches (az_timing: every 8th simulation step)
-    sel_bytes_per_launch = tm["select_bytes"] / max(args.steps * S, 1)
+    sel_bytes_per_launch = tm["select_bytes"] / max(args.steps * K, 1)
     sel_ms_per_launch = tm["select_ms"] / max(tm["select_launches"], 1)
     sel_gbs = sel_bytes_per_launch / (sel_ms_per_launch * 1e-3) / 1e9 if tm["select_ms"] > 0 else 0.0
     out = {
@@ -283,26 +435,22 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": args.dtype,
-        "data": "synthetic: random-init %dx%d weights (seed 42), self-play from startpos, Dirichlet noise on"
-                % (args.blocks, args.filters),
+        "data": ("rehearsal: CPU stub engine, no GPU -- exercises the rank plumbing only, the numbers measure nothing"
+                 if args.rehearse else
+                 "synthetic: random-init %dx%d weights (seed 42), self-play from startpos, Dirichlet noise on"
+                 % (args.blocks, args.filters)),
         "config": {"workload": "%s: %d concurrent self-play games/GPU x %d sims/move, %d-block x %d-filter net"
                                % (config_name(G, S, args.blocks, args.filters), G, S, args.blocks, args.filters),
                    "games_per_gpu": G, "sims_per_move": S, "blocks": args.blocks, "filters": args.filters,
-                   "fen_cache": "off for value (see with_fen_cache)",
+                   "sims_per_step": K,
+                   "step": "%d simulation steps of every game (a move = %d steps)" % (K, S // K),
+                   "fen_cache": "off (measured: 1 % hit rate over a 20-move C3 window, -14 % at C2; DESIGN.md section 6)",
                    "parallelism": "games sharded %d-way, no collective (gloo barrier/max only)" % world},
-        "roofline": {"bound": "mfma", "achieved": conv_tflops, "peak": peak, "unit": "TFLOP/s",
-                     "frac": conv_tflops / peak, "traffic": traffic,
-                     "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
-                     "kernel": ("tower_kernel<%d> (fused input conv + %d residual convs + heads; algorithmic "
-                                "FLOPs = conv FLOPs only), %d launches timed (HIP events on every 8th simulation step)" % (args.filters, 2 * args.blocks,
-                                                                                 tm["conv_launches"]))
-                               if net.fused_tower else
-                               "conv3x3_kernel<%d,%d> (residual 3x3 conv), %d launches timed" %
-                               (args.filters, args.filters, tm["conv_launches"]),
-                     "flop_per_launch": tm["conv_flop"] / max(tm["conv_launches"], 1),
-                     "avg_ms_per_launch": tm["conv_ms"] / max(tm["conv_launches"], 1)},
+        "roofline": roofline(tm, args.dtype, fused),
         "tower": {"achieved_tflops": tower_tflops, "frac": tower_tflops / peak,
                   "ms_per_sim_step": tm["tower_ms"] / max(tm["sim_steps"], 1)},
+        "tolerance_vs_f32_oracle": TOLERANCE[args.dtype],
+        "bf16_mode": bf16_res,
         "tree_walk": {"kernel": "k_select", "achieved_gbs": sel_gbs, "peak_gbs": PEAK_HBM_GBS,
                       "frac": sel_gbs / PEAK_HBM_GBS,
                       "bytes_per_sim": tm["select_bytes"] / max(sims_rank, 1),
@@ -319,7 +467,7 @@ def main():
         "cpu_baseline": None,
         "training": training,
     }
-    if (args.blocks, args.filters, S) == (20, 256, 800) and os.path.exists(GAME_LENGTH):
+    if (args.blocks, args.filters, S) == (20, 256, 800) and os.path.exists(GAME_LENGTH) and not args.rehearse:
         with open(GAME_LENGTH) as f:
             gl = json.load(f)
         # continuous self-play keeps every slot busy (a finished game restarts in its slot), so
@@ -327,9 +475,10 @@ def main():
         out["games_per_hr_projected"] = {
             "value": value * 3600.0 / (S * gl["plies_mean"]), "plies_per_game": gl["plies_mean"],
             "source": os.path.relpath(GAME_LENGTH, ROOT),
-            "note": "steady-state continuous self-play: measured sims/s / (800 sims x mean plies of %d complete "
-                    "games); the timed window is %d moves, too short for games to finish" % (gl["games"], args.steps)}
-    if world == 1 and not args.no_cpu_baseline:
+            "note": "projection, not a measurement: measured sims/s / (800 sims x mean plies of %d complete games "
+                    "of a separate run); the timed window (%d x %d simulation steps) is too short for games to "
+                    "finish" % (gl["games"], args.steps, K)}
+    if world == 1 and not args.no_cpu_baseline and not args.rehearse:
         out["cpu_baseline"] = cpu_baseline(args.blocks, args.filters, args.cpu_threads, args.cpu_games,
                                            args.cpu_sims)
     print(json.dumps(out))
@@ -338,4 +487,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

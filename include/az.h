@@ -140,6 +140,12 @@ int az_selfplay_reset(az_search* s);
 /* one move for every active game: sims, improved policy, action choice (training.rs:310-321),
  * play, traverse/record.  *finished = games that ended in this step. */
 int az_selfplay_step(az_search* s, int* finished, int* active);
+/* The same move in pieces: the next `nsims` simulation steps of every game's current move
+ * (async_monte_carlo_tree_search's loop, tree.rs:169-178, cut at any simulation boundary).
+ * When the move's sims are complete (*move_done = 1) the action choice, play and re-root of
+ * az_selfplay_step follow; until then *finished = 0, *active = -1.  Results are identical to
+ * az_selfplay_step. */
+int az_selfplay_run_sims(az_search* s, int nsims, int* finished, int* active, int* move_done);
 
 /* EpisodeStep (training.rs:15-20) of finished games, drained in game order. */
 typedef struct {
@@ -165,6 +171,10 @@ typedef struct {
     int64_t max_depth_sum;     /* sum over moves of max_subtree_depth */
     int64_t cache_hits;        /* expansions served by the FEN cache (CACHE_HITS, training.rs:12) */
     int64_t cache_misses;      /* expansions that needed a network row (CACHE_MISSES) */
+    int64_t overflow;          /* expansions refused for want of node/edge arena space (0 by construction) */
+    int64_t max_nodes;         /* largest node count of any game's current tree (arena: sims + 2) */
+    int64_t max_edges;         /* largest edge count of any game's current tree */
+    int64_t node_cap, edge_cap;/* the per-game arena sizes */
 } az_search_stats;
 int az_search_stats_get(az_search* s, az_search_stats* out);
 

@@ -34,4 +34,5 @@ def test_python_binding_covers_header():
 def test_struct_sizes():
     import azchess._lib as L
     assert ctypes.sizeof(L.AzPos) == 80
+    assert ctypes.sizeof(L.AzSearchStats) == 13 * 8
     assert ctypes.sizeof(L.AzEpisodeStep) == 32 + 80 + 2 * 224 * 2  # az_pos 8-byte aligned

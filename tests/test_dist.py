@@ -48,3 +48,39 @@ def test_two_rank_gloo_sharding_and_reduction():
     for r in res:
         assert r[3] == 2.0                           # max over ranks
         assert r[4] == [2 * 2048 * 800 * 3, 2 * 2048 * 800 * 3 - 1, 1]
+
+
+def _bench(args, env=None, timeout=240):
+    import json
+    import subprocess
+    import sys
+    from conftest import ROOT
+    e = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                         timeout=timeout, env=e)
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    return out.returncode, [json.loads(l) for l in lines], out.stderr
+
+
+def test_bench_gpus_flag_spawns_the_ranks():
+    """`bench.py --gpus 2` with no torchrun environment starts 2 ranks itself (the same code path
+    a GPU run takes, with the CPU stub engine): one JSON line from rank 0, n_gpus = 2, value =
+    the simulations of BOTH ranks / the max-over-ranks time."""
+    G, K, steps = 64, 8, 3
+    rc, lines, err = _bench(["--gpus", "2", "--rehearse", "--steps", str(steps), "--warmup", "1", "--games", str(G),
+                             "--sims", "16", "--sims-per-step", str(K), "--bf16-steps", "0"])
+    assert rc == 0, err[-2000:]
+    assert len(lines) == 1
+    r = lines[0]
+    assert r["n_gpus"] == 2 and r["steps"] == steps and r["scaling"] == "weak"
+    sims = r["value"] * r["ms_per_step"] * 1e-3 * steps
+    assert abs(sims - 2 * G * K * steps) < 1e-6 * sims
+    assert "2-way" in r["config"]["parallelism"]
+
+
+def test_bench_rejects_world_mismatch():
+    rc, lines, err = _bench(["--gpus", "1", "--rehearse", "--steps", "1"], env={"WORLD_SIZE": "2", "RANK": "0"})
+    assert rc != 0 and not lines and "WORLD_SIZE=2" in err

@@ -55,6 +55,7 @@ def random_planes(n, seed):
 
 
 @pytest.mark.parametrize("blocks,filters,dtype,n", [(6, 64, "f32", 24), (6, 64, "bf16", 24), (2, 128, "bf16", 9),
+                                                    (2, 128, "f32", 9), (2, 32, "f32", 17),
                                                     (20, 256, "bf16", 6), (20, 256, "f32", 6)])
 def test_net_matches_oracle(require_gpu, blocks, filters, dtype, n):
     w = A.random_weights(blocks, filters, seed=42)
@@ -80,22 +81,28 @@ def test_rows_are_batch_independent(require_gpu, dtype):
     assert np.array_equal(p2[:6], pol[7:]) and np.array_equal(v2[6:], val[:7])
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
 @pytest.mark.parametrize("blocks,filters", [(2, 32), (6, 64), (2, 128), (20, 256)])
-def test_fused_tower_matches_per_layer_kernels(require_gpu, blocks, filters, monkeypatch):
-    """tower_kernel (whole tower + heads in one launch, activations resident in LDS) against
-    the per-layer conv3x3_kernel + heads_kernel path on the same bf16 weights."""
+def test_fused_tower_matches_per_layer_kernels(require_gpu, blocks, filters, dtype, monkeypatch):
+    """tower_kernel / tower32_kernel (whole tower + heads in one launch, activations resident
+    in LDS) against the per-layer conv3x3_kernel + heads_kernel path on the same weights."""
     w = A.random_weights(blocks, filters, seed=7)
     planes = random_planes(37, 11)
     monkeypatch.setenv("AZ_FUSED_TOWER", "1")
-    fused = A.AlphaZero(blocks, filters, weights=w, dtype="bf16")
+    fused = A.AlphaZero(blocks, filters, weights=w, dtype=dtype)
     pf, vf = fused.forward(planes)
     monkeypatch.setenv("AZ_FUSED_TOWER", "0")
-    layered = A.AlphaZero(blocks, filters, weights=w, dtype="bf16")
+    layered = A.AlphaZero(blocks, filters, weights=w, dtype=dtype)
     pl, vl = layered.forward(planes)
-    # same bf16 arithmetic, but the fused path adds the bias before the K sum (accumulator init):
-    # occasional bf16 rounding flips -> bf16-scale tolerance (each path is also checked vs the oracle)
-    np.testing.assert_allclose(vf, vl, atol=2e-3)
-    np.testing.assert_allclose(pf, pl, rtol=2e-2, atol=1e-6)
+    if dtype == "bf16":
+        # same bf16 arithmetic, but the fused path adds the bias before the K sum (accumulator
+        # init): occasional bf16 rounding flips -> bf16-scale tolerance
+        np.testing.assert_allclose(vf, vl, atol=2e-3)
+        np.testing.assert_allclose(pf, pl, rtol=2e-2, atol=1e-6)
+    else:
+        # f32: same products, bias added first vs last and MFMA vs VALU heads -> f32 rounding only
+        np.testing.assert_allclose(vf, vl, atol=1e-5)
+        np.testing.assert_allclose(pf, pl, rtol=1e-4, atol=1e-8)
 
 
 def test_mpk_model_file_drives_the_engine(require_gpu, tmp_path):

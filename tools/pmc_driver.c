@@ -4,7 +4,7 @@
  * tower in search mode once, exactly as bench.py's timed region does.
  * Weights: the flat f32 layout of az_net_num_params, written by
  *   python3 -c "import azchess as A; A.random_weights(20, 256, seed=42).tofile('w.f32')"
- * Build: make -C tools   Run: tools/pmc_driver games sims moves blocks filters w.f32 */
+ * Build: make -C tools   Run: tools/pmc_driver games sims moves blocks filters w.f32 [f32|bf16] */
 #include <stdio.h>
 #include <stdlib.h>
 #include <time.h>
@@ -22,7 +22,8 @@ int main(int argc, char** argv) {
     FILE* f = fopen(argv[6], "rb");
     if (!f || fread(w, sizeof(float), n, f) != n) { fprintf(stderr, "cannot read %zu weights from %s\n", n, argv[6]); return 1; }
     fclose(f);
-    az_net_desc d = {blocks, filters, AZ_DTYPE_BF16};
+    const int bf = argc > 7 && argv[7][0] == 'b';
+    az_net_desc d = {blocks, filters, bf ? AZ_DTYPE_BF16 : AZ_DTYPE_F32};
     az_net* net;
     CHECK(az_net_create(&d, w, n, 0, &net));
     az_search_cfg cfg;
@@ -38,8 +39,8 @@ int main(int argc, char** argv) {
     CHECK(az_device_synchronize(0));
     clock_gettime(CLOCK_MONOTONIC, &t1);
     double dt = (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
-    printf("pmc_driver: %d games x %d sims x %d moves, %dx%d bf16: %.3f s (%.0f sims/s)\n", games, sims, moves, blocks,
-           filters, dt, (double)games * sims * moves / dt);
+    printf("pmc_driver: %d games x %d sims x %d moves, %dx%d %s: %.3f s (%.0f sims/s)\n", games, sims, moves, blocks,
+           filters, bf ? "bf16" : "f32", dt, (double)games * sims * moves / dt);
     az_search_destroy(sp);
     az_net_destroy(net);
     free(w);

@@ -1,7 +1,8 @@
 """Summarise tools/pmc_run.sh output for one kernel (per-launch averages).
 HBM bytes per MI355X_MICROARCH.md 'HBM': FETCH_SIZE reads half the bytes of wide coalesced
 streaming reads on gfx950 (x2 correction), WRITE_SIZE exact for 16-B stores; both in KB.
-Usage: python tools/pmc_summary.py <outdir> [kernel-name substring, default tower_kernel]"""
+Usage: python tools/pmc_summary.py <outdir> [kernel-name substring, default tower_kernel] [MFMA cycles/SIMD:
+16 for v_mfma_f32_16x16x32_bf16 (default), 32 for v_mfma_f32_16x16x4_f32]"""
 import collections
 import csv
 import glob
@@ -11,6 +12,7 @@ import sys
 
 d = sys.argv[1]
 pat = sys.argv[2] if len(sys.argv) > 2 else "tower_kernel"
+mfma_cyc = float(sys.argv[3]) if len(sys.argv) > 3 else 16.0
 res = {"kernel_pattern": pat}
 durs = []
 for sub in ("fetch", "write", "sq", "cyc"):
@@ -45,6 +47,6 @@ if "SQ_WAVE_CYCLES" in res:
     if durs:
         res["effective_clock_ghz"] = res["GRBM_GUI_ACTIVE"] / 8 / res["profiled_avg_launch_s"] / 1e9
 if "SQ_INSTS_MFMA" in res and "GRBM_GUI_ACTIVE" in res:
-    # v_mfma_f32_16x16x32_bf16 = 16 cycles (MI355X_MICROARCH.md cycle constants)
-    res["mfma_issue_frac"] = res["SQ_INSTS_MFMA"] * 16 / (res["GRBM_GUI_ACTIVE"] / 8 * 1024)
+    # v_mfma_f32_16x16x32_bf16 = 16 cycles, v_mfma_f32_16x16x4_f32 = 32 (MI355X_MICROARCH.md cycle constants)
+    res["mfma_issue_frac"] = res["SQ_INSTS_MFMA"] * mfma_cyc / (res["GRBM_GUI_ACTIVE"] / 8 * 1024)
 print(json.dumps(res, indent=1))

@@ -66,7 +66,8 @@ int main(int argc, char** argv) {
     for (int r = 0; r < ROUNDS; r++) {
         for (int i = 0; i < nlib; i++) {
             lib_t* L = &libs[i];
-            az_net_desc d = {blocks, filters, AZ_DTYPE_BF16};
+            const char* dt = getenv("DTYPE");
+            az_net_desc d = {blocks, filters, dt && dt[0] == 'b' ? AZ_DTYPE_BF16 : AZ_DTYPE_F32};
             az_net* net;
             CHECK(L, L->net_create(&d, w, n, 0, &net));
             az_search_cfg cfg;
