@@ -23,6 +23,21 @@ int fail(const std::string& msg);
             return ::azi::fail(std::string(#expr) + ": " + hipGetErrorString(e_));          \
     } while (0)
 
+// ---------------- loads of state another launch rewrote ----------------
+// A load at a provably wave-uniform address compiles to s_load, which goes through the scalar
+// data cache; measured on MI355X (round 2): that cache can still hold the line a previous launch
+// of the stream read, so vector stores made in between are not seen (k_expand read stale leaf
+// records).  Engine state that launches hand to each other (batch counters, row -> game maps,
+// per-game records) is therefore read through vector loads: load_fresh for a single counter,
+// vgpr_index for an index that would otherwise make every load behind it scalar.
+__device__ __forceinline__ int load_fresh(const int* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int vgpr_index(int i) {
+    asm volatile("" : "+v"(i));
+    return i;
+}
+
 // ---------------- search tree records (HBM, struct-of-arrays per game) ----------------
 struct Node {            // 16 B
     uint32_t edge_begin; // first edge (game-relative)

@@ -65,7 +65,7 @@ conv3x3_kernel(const T* __restrict__ in, T* __restrict__ out, const void* __rest
     constexpr int ZN = 16 + NSLOT;
     __shared__ __attribute__((aligned(16))) uint4 lds[ZB + ZN];
 
-    const int count = count_ptr ? min(*count_ptr, rows) : rows;
+    const int count = count_ptr ? min(load_fresh(count_ptr), rows) : rows;
     const int row0 = blockIdx.x * BPB;
     if (row0 >= count) return;
     const int nb = min(BPB, count - row0);
@@ -200,8 +200,8 @@ heads_kernel(const T* __restrict__ x, const float* __restrict__ head, const int*
     __shared__ float v1[8 * 64];
     __shared__ float red[4 * 64];
     __shared__ float stat[8];
-    const int count = count_ptr ? min(*count_ptr, rows) : rows;
-    const int row = blockIdx.x;
+    const int count = count_ptr ? min(load_fresh(count_ptr), rows) : rows;
+    const int row = vgpr_index(blockIdx.x);
     if (row >= count) return;
     const int tid = threadIdx.x;
     const HeadLayout L = HeadLayout::make(F);
@@ -314,8 +314,8 @@ template <typename T>
 __global__ void encode_rows_kernel(const azc::Pos* __restrict__ npos, int NMAX, const int* __restrict__ row_game,
                                    const int* __restrict__ row_node, const int* __restrict__ count_ptr, int rows,
                                    T* __restrict__ planes) {
-    const int row = blockIdx.x;
-    const int count = count_ptr ? min(*count_ptr, rows) : rows;
+    const int row = vgpr_index(blockIdx.x);
+    const int count = count_ptr ? min(load_fresh(count_ptr), rows) : rows;
     if (row >= count) return;
     const int sq = threadIdx.x;
     const azc::Pos p = npos[(size_t)row_game[row] * NMAX + row_node[row]];
@@ -336,7 +336,7 @@ __global__ void planes_from_nchw_kernel(const float* __restrict__ in, int rows, 
 // synthetic evaluator -- the same definition the oracle uses
 __global__ void synth_eval_kernel(const int* __restrict__ count_ptr, int rows, SearchOut so) {
     const int row = blockIdx.x * blockDim.x + threadIdx.x;
-    const int count = count_ptr ? min(*count_ptr, rows) : rows;
+    const int count = count_ptr ? min(load_fresh(count_ptr), rows) : rows;
     if (row >= count) return;
     const int game = so.row_game[row], node = so.row_node[row];
     const Node nd = so.nodes[(size_t)game * so.NMAX + node];

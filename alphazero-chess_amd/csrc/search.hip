@@ -111,7 +111,7 @@ __device__ __forceinline__ bool same_fen(const azc::Pos& a, const azc::Pos& b) {
 // insert every row just evaluated by the network (process_batch's cache.insert, training.rs:413)
 __global__ void __launch_bounds__(64) k_cache_insert(Engine E, int step) {
     const int row = blockIdx.x * blockDim.x + threadIdx.x;
-    if (row >= *step_rows(E, step)) return;
+    if (row >= load_fresh(step_rows(E, step))) return;
     const int g = E.row_game[row], node = E.row_node[row];
     const azc::Pos p = E.npos[(size_t)g * E.NMAX + node];
     const Node nd = E.nodes[(size_t)g * E.NMAX + node];
@@ -231,6 +231,232 @@ __device__ __forceinline__ int expand_leaf(const Engine& E, int g, int* nid_out)
     return X_ROW;
 }
 
+// ------------------------------------------------------------------ wave-parallel expansion
+// The same expansion with the 64 lanes of a wavefront (one game per wave): the legal-move list
+// of the new leaf in shakmaty order (azc::gen_legal's order), generated by
+// square -- lane s owns square s (the from-square; the to-square for pawn pushes) -- with one
+// wave prefix sum per generation group giving every move its position; the repetition count
+// compares one earlier position per lane.  Every value a branch depends on is wave-uniform.
+#ifndef AZ_EXPAND_WAVE
+#define AZ_EXPAND_WAVE 1   // 0: the one-lane serial expansion (A/B)
+#endif
+__device__ __forceinline__ int wave_scan_incl(int v, int lane) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ int gen_legal_wave(const azc::Pos& p, Edge* __restrict__ out, int lane, bool* in_check,
+                                           bool* legal_ep) {
+    using namespace azc;
+    const int us = p.turn, them = us ^ 1;
+    const uint64_t our = p.bb[WHITE_BB + us], their = p.bb[WHITE_BB + them];
+    const uint64_t occ = our | their, empty = ~occ;
+    const uint64_t kbb = p.bb[KING] & our;
+    const int ksq = ctz64(kbb);
+    const uint64_t tP = p.bb[PAWN] & their, tN = p.bb[KNIGHT] & their, tK = p.bb[KING] & their;
+    const uint64_t tB = (p.bb[BISHOP] | p.bb[QUEEN]) & their, tR = (p.bb[ROOK] | p.bb[QUEEN]) & their;
+    const uint64_t checkers = (pawn_att(us, kbb) & tP) | (knight_att(kbb) & tN) | (bishop_att(kbb, empty) & tB) |
+                              (rook_att(kbb, empty) & tR);
+    const uint64_t empty_xk = empty | kbb;
+    const uint64_t attacked = pawn_att(them, tP) | knight_att(tN) | king_att(tK) | bishop_att(tB, empty_xk) |
+                              rook_att(tR, empty_xk);
+    uint64_t pinned = 0, pinray[8], checkmask = checkers;
+#pragma unroll
+    for (int d = 0; d < 8; d++) {
+        const uint64_t r = ray_dir(d, kbb, empty);
+        const uint64_t sl = (d & 1) ? tB : tR;
+        pinray[d] = 0;
+        if (r & checkers & sl) checkmask |= r;
+        const uint64_t blk = r & our;
+        if (blk) {
+            const uint64_t r2 = ray_dir(d, kbb, empty | blk);
+            if (r2 & sl & ~r) { pinned |= blk; pinray[d] = r2; }
+        }
+    }
+    auto allowed = [&](int from) -> uint64_t {
+        if (!((pinned >> from) & 1)) return ALL;
+        uint64_t r = 0;
+#pragma unroll
+        for (int d = 0; d < 8; d++) r = ((pinray[d] >> from) & 1) && !r ? pinray[d] : r;
+        return r;
+    };
+    const uint64_t sb = 1ULL << lane;
+    int base = 0;
+    // one generation group: this lane's targets t (ascending to-squares) from square `from`
+    auto emit = [&](uint64_t t, int from, int flag) {
+        const int cnt = popc64(t);
+        if (__ballot(cnt != 0) == 0) return;
+        const int incl = wave_scan_incl(cnt, lane);
+        int pos = base + incl - cnt;
+        while (t) {
+            const int to = ctz64(t);
+            t &= t - 1;
+            Edge e;
+            e.P = 0.0f; e.W = 0.0f; e.N = 0; e.idx = (uint16_t)(move_index(from, to, us) | flag); e.child = CHILD_NONE;
+            out[pos++] = e;
+        }
+        base += __shfl(incl, 63, 64);
+    };
+    *in_check = checkers != 0;
+    *legal_ep = false;
+    if (p.ep < 64) {                                   // en passant first, full attack test
+        const uint64_t epbb = 1ULL << p.ep;
+        const int capsq = us == 0 ? p.ep - 8 : p.ep + 8;
+        const uint64_t capbb = 1ULL << capsq;
+        const uint64_t fr = p.bb[PAWN] & our & pawn_att(them, epbb);
+        uint64_t t = 0;
+        if ((fr >> lane) & 1) {
+            const uint64_t occ2 = (occ ^ sb ^ capbb) | epbb;
+            const uint64_t att2 = (rook_att(kbb, ~occ2) & tR) | (bishop_att(kbb, ~occ2) & tB) |
+                                  (knight_att(kbb) & tN) | (pawn_att(us, kbb) & tP & ~capbb);
+            if (!att2) t = epbb;
+        }
+        *legal_ep = __ballot(t != 0) != 0;
+        emit(t, lane, 0);
+    }
+    const int nchk = popc64(checkers);
+    auto non_king = [&](uint64_t target) {
+        const uint64_t ourP = p.bb[PAWN] & our;
+        const uint64_t seventh = ourP & (us == 0 ? (0xFFULL << 48) : (0xFFULL << 8));
+        const uint64_t patt = pawn_att(us, sb) & their & target;
+        emit(((ourP & ~seventh) >> lane) & 1 ? patt & allowed(lane) : 0, lane, 0);          // captures
+        emit((seventh >> lane) & 1 ? patt & allowed(lane) : 0, lane, PROMO_FLAG);          // capture promotions
+        const uint64_t single = (us == 0 ? (ourP << 8) : (ourP >> 8)) & empty;
+        const uint64_t dbl = (us == 0 ? (single << 8) & (0xFFULL << 24) : (single >> 8) & (0xFFULL << 32)) & empty;
+        const int f1 = us == 0 ? lane - 8 : lane + 8, f2 = us == 0 ? lane - 16 : lane + 16;   // pushes: lane = to
+        const bool s1 = ((single & target) >> lane) & 1, s2 = ((dbl & target) >> lane) & 1;
+        const bool ok1 = s1 && ((allowed(f1 & 63) >> lane) & 1);
+        const bool ok2 = s2 && ((allowed(f2 & 63) >> lane) & 1);
+        emit(ok1 && !((BACKRANKS >> lane) & 1) ? sb : 0, f1, 0);                           // single pushes
+        emit(ok1 && ((BACKRANKS >> lane) & 1) ? sb : 0, f1, PROMO_FLAG);                   // push promotions
+        emit(ok2 ? sb : 0, f2, 0);                                                          // double pushes
+        emit(((p.bb[KNIGHT] & our & ~pinned) >> lane) & 1 ? knight_att(sb) & target : 0, lane, 0);
+        emit(((p.bb[BISHOP] & our) >> lane) & 1 ? bishop_att(sb, empty) & target & allowed(lane) : 0, lane, 0);
+        emit(((p.bb[ROOK] & our) >> lane) & 1 ? rook_att(sb, empty) & target & allowed(lane) : 0, lane, 0);
+        emit(((p.bb[QUEEN] & our) >> lane) & 1
+                 ? (bishop_att(sb, empty) | rook_att(sb, empty)) & target & allowed(lane) : 0, lane, 0);
+    };
+    const uint64_t kt = lane == ksq ? king_att(kbb) & ~our & ~attacked : 0;
+    if (nchk == 0) {
+        non_king(~our);
+        emit(kt, ksq, 0);
+        const int home = us == 0 ? 0 : 56;
+        const uint8_t kbit = us == 0 ? 1 : 4, qbit = us == 0 ? 2 : 8;
+        const bool oo = (p.castling & kbit) && ksq == home + 4 && ((p.bb[ROOK] & our) >> (home + 7) & 1) &&
+                        !(occ & (3ULL << (home + 5))) && !(attacked & (7ULL << (home + 4)));
+        const bool ooo = (p.castling & qbit) && ksq == home + 4 && ((p.bb[ROOK] & our) >> home & 1) &&
+                         !(occ & (7ULL << (home + 1))) && !(attacked & (7ULL << (home + 2)));
+        emit(lane == 0 && oo ? 1ULL << (home + 7) : 0, ksq, 0);
+        emit(lane == 0 && ooo ? 1ULL << home : 0, ksq, 0);
+    } else {
+        emit(kt, ksq, 0);
+        if (nchk == 1) non_king(checkmask);
+    }
+    return base;
+}
+
+__device__ __forceinline__ int expand_leaf_wave(const Engine& E, int g, int lane, int* nid_out) {
+    // g is wave-uniform, and a provably uniform index would turn the per-game loads below into
+    // scalar (s_load) reads; the leaf records were written by vector stores of another launch
+    // (k_select), which the scalar cache does not see -- keep g in a VGPR so they stay vector loads
+    g = vgpr_index(g);
+    if (g >= E.G || !E.active[g] || E.leaf_kind[g] != LEAF_EVAL) return X_NONE;
+    Node* nodes = game_nodes(E, g);
+    Edge* edges = game_edges(E, g);
+    azc::Pos* npos = game_npos(E, g);
+    const int parent = E.leaf_node[g], eabs = E.leaf_edge[g];
+    const int idx = edges[eabs].idx & azc::IDX_MASK;
+    const azc::Pos pp = npos[parent];
+    const int ebeg = E.edge_count[g];
+    const int nid = E.node_count[g];
+    const int pdepth = nodes[parent].depth;
+    const int maxd = E.max_depth[g];
+    const int hlen = E.hist_len[g];
+    const int plen = E.leaf_len[g];
+    const int* pn = E.path_node + (size_t)g * E.PMAX;
+    azc::Pos c = azc::play_index(pp, idx);
+    bool chk = false, lep = false;
+    const int n = gen_legal_wave(c, edges + ebeg, lane, &chk, &lep);
+    c.flags = lep ? 1 : 0;
+    c.rep_key = azc::rep_key_of(c);
+    int res = azc::outcome(c, n, chk);
+    if (res == azc::ONGOING) {
+        // earlier positions d plies back, d even, d <= halfmoves: d <= plen on the tree path
+        // (pn[plen - d]), beyond it in the game history -- one candidate per lane
+        const int hm = c.halfmoves;
+        int cnt = 0;
+        for (int d0 = 2; d0 <= hm; d0 += 128) {
+            const int d = d0 + 2 * lane;
+            bool eq = false;
+            if (d <= hm) {
+                if (d <= plen) eq = azc::chess_eq(npos[pn[plen - d]], c);
+                else {
+                    const int hi = hlen - 1 - d + plen;
+                    if (hi >= 0) eq = azc::chess_eq(E.hist[(size_t)g * HMAX + hi], c);
+                }
+            }
+            cnt += __popcll(__ballot(eq));
+        }
+        if (cnt + 1 >= azc::REPETITIONS || c.halfmoves >= azc::NUM_HALFMOVES || c.fullmoves >= azc::NUM_FULLMOVES)
+            res = azc::DRAW;
+    }
+    if (res != azc::ONGOING) {
+        if (lane == 0) {
+            edges[eabs].child = res == azc::DRAW ? CHILD_DRAW : CHILD_WIN;
+            E.leaf_kind[g] = res == azc::DRAW ? LEAF_DRAW : LEAF_WIN;
+        }
+        return X_TERMINAL;
+    }
+    if (nid >= E.NMAX || ebeg + n > E.EMAX) {
+        if (lane == 0) {
+            E.leaf_kind[g] = LEAF_DRAW;
+            atomicAdd(&E.ctr->overflow, 1);
+        }
+        return X_NONE;
+    }
+    if (lane == 0) {
+        Node nn;
+        nn.edge_begin = (uint32_t)ebeg;
+        nn.nedges = (uint16_t)n;
+        nn.depth = (uint16_t)(pdepth + 1);
+        nn.nsum = 0;
+        nn.parent = parent;
+        nodes[nid] = nn;
+        npos[nid] = c;
+        E.node_count[g] = nid + 1;
+        E.edge_count[g] = ebeg + n;
+        edges[eabs].child = nid;
+        if (nn.depth > maxd) E.max_depth[g] = nn.depth;
+    }
+    if (E.cache_mask >= 0) {                                 // FEN cache lookup (tree.rs:214-219): probe = lane
+        const uint64_t key = azc::fen_key(c);
+        bool hit = false;
+        int sl = 0;
+        if (lane < CACHE_PROBES) {
+            sl = (int)((key + (uint64_t)lane) & (uint64_t)E.cache_mask);
+            hit = E.c_state[sl] == 2u && E.c_key[sl] == key && E.c_n[sl] == n && same_fen(E.c_pos[sl], c);
+        }
+        const unsigned long long hm = __ballot(hit);
+        if (hm) {
+            const int first = __builtin_ctzll(hm);
+            sl = __shfl(sl, first, 64);
+            const float* pri = E.c_pri + (size_t)sl * MAX_EDGES;
+            for (int e = lane; e < n; e += 64) edges[ebeg + e].P = pri[e];
+            if (lane == 0) {
+                E.cached_value[g] = E.c_value[sl];
+                E.leaf_kind[g] = LEAF_CACHED;
+            }
+            return X_CACHED;
+        }
+    }
+    *nid_out = nid;
+    return X_ROW;
+}
+
 // AZ_EXPAND_GPW games per wavefront (lanes >= GPW idle): the per-lane expansion is serial,
 // branchy integer code, so fewer games per wave means less divergence and more CUs in use.
 // Row allocation and the counters are one atomic per wave (ballot + popcount), not per game.
@@ -239,6 +465,23 @@ __device__ __forceinline__ int expand_leaf(const Engine& E, int g, int* nid_out)
 #endif
 __global__ void __launch_bounds__(64) k_expand(Engine E, int step) {
     const int lane = threadIdx.x;
+#if AZ_EXPAND_WAVE
+    const int g = vgpr_index(blockIdx.x);
+    int nid = -1;
+    const int kind = expand_leaf_wave(E, g, lane, &nid);
+    if (lane == 0) {
+        if (kind == X_ROW) {
+            const int row = atomicAdd(step_rows(E, step), 1);
+            E.row_game[row] = g;
+            E.row_node[row] = nid;
+            E.leaf_row[g] = row;
+        } else if (kind == X_TERMINAL) {
+            atomicAdd(&E.ctr->terminal, 1ull);
+        } else if (kind == X_CACHED) {
+            atomicAdd(&E.ctr->cache_hits, 1ull);
+        }
+    }
+#else
     const int g = lane < AZ_EXPAND_GPW ? blockIdx.x * AZ_EXPAND_GPW + lane : E.G;
     int nid = -1;
     const int kind = expand_leaf(E, g, &nid);
@@ -258,6 +501,7 @@ __global__ void __launch_bounds__(64) k_expand(Engine E, int step) {
     const unsigned long long mt = __ballot(kind == X_TERMINAL), mc = __ballot(kind == X_CACHED);
     if (lane == 0 && mt) atomicAdd(&E.ctr->terminal, (unsigned long long)__popcll(mt));
     if (lane == 0 && mc) atomicAdd(&E.ctr->cache_hits, (unsigned long long)__popcll(mc));
+#endif
 }
 
 // ------------------------------------------------------------------ backup
@@ -265,7 +509,7 @@ __global__ void __launch_bounds__(64) k_expand(Engine E, int step) {
 // cleared for step + 2
 __device__ __forceinline__ void backup_stats(const Engine& E, int step) {
     int* rows = step_rows(E, step);
-    const int n = *rows;
+    const int n = load_fresh(rows);
     atomicAdd(&E.ctr->evals, (unsigned long long)n);
     if (step >= 0 && step < E.S) E.batch_hist[step] = n;
     *rows = 0;
@@ -321,7 +565,11 @@ __global__ void __launch_bounds__(STEP_WPB * 64) k_step(Engine E, int step, int 
     if (live) {
         select_game(E, g, lane);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+#if AZ_EXPAND_WAVE
+        kind = expand_leaf_wave(E, g, lane, &nid);
+#else
         if (lane == 0) kind = expand_leaf(E, g, &nid);
+#endif
     }
     if (lane == 0) { s_kind[w] = kind; s_nid[w] = nid; }
     __syncthreads();
@@ -405,14 +653,14 @@ __global__ void __launch_bounds__(64) k_root_noise(Engine E, int apply) {
     __shared__ float gam[AZ_MAX_MOVES];
     __shared__ int kpos[MAX_EDGES + 1];
     __shared__ float sh[2];
-    const int g = blockIdx.x;
+    const int g = vgpr_index(blockIdx.x);
     if (g >= E.G || !E.active[g] || !apply) return;
     root_noise(E, g, E.game_id[g], E.ply[g], gam, kpos, sh);
 }
 
 __global__ void k_save_start_template(Engine E) {   // game 0's un-noised startpos root
-    const Edge* edges = game_edges(E, 0);
-    const int n = game_nodes(E, 0)[0].nedges;
+    const Edge* edges = game_edges(E, vgpr_index(0));
+    const int n = game_nodes(E, vgpr_index(0))[0].nedges;
     for (int e = threadIdx.x; e < n; e += blockDim.x) E.start_edges[e] = edges[e];
     if (threadIdx.x == 0) *E.start_n = n;
 }
@@ -427,7 +675,7 @@ __global__ void __launch_bounds__(64) k_finish(Engine E, int mode, const int* ac
     __shared__ int kpos[MAX_EDGES + 1];
     __shared__ float sh[2];
     __shared__ int si[4];
-    const int g = blockIdx.x, lane = threadIdx.x;
+    const int g = vgpr_index(blockIdx.x), lane = threadIdx.x;
     if (g >= E.G || !E.active[g]) return;
     Node* nodes = game_nodes(E, g);
     Edge* edges = game_edges(E, g);
@@ -569,7 +817,7 @@ __global__ void __launch_bounds__(64) k_finish(Engine E, int mode, const int* ac
     if (lane == 0) si[3] = atomicAdd(&E.ctr->next_game_id, 1);
     __syncthreads();
     const int ngid = si[3];
-    const int sn = *E.start_n;
+    const int sn = load_fresh(E.start_n);
     for (int e = lane; e < sn; e += 64) edges[e] = E.start_edges[e];
     if (lane == 0) {
         const azc::Pos sp = azc::startpos();
@@ -591,7 +839,7 @@ __global__ void __launch_bounds__(64) k_finish(Engine E, int mode, const int* ac
 
 // visits / improved policy / depth readout (dense 4096 per game)
 __global__ void k_readout(Engine E, float* improved, uint32_t* visits, int* depth) {
-    const int g = blockIdx.x;
+    const int g = vgpr_index(blockIdx.x);
     if (g >= E.G) return;
     const Node r = game_nodes(E, g)[0];
     const Edge* edges = game_edges(E, g);
@@ -712,7 +960,7 @@ int sim_step(az_search* s, int step, hipEvent_t* ev) {
     if (ev) (void)hipEventRecord(ev[0], st);
     k_select<<<(G * 64 + 255) / 256, 256, 0, st>>>(E);
     if (ev) (void)hipEventRecord(ev[1], st);
-    k_expand<<<(G + AZ_EXPAND_GPW - 1) / AZ_EXPAND_GPW, 64, 0, st>>>(E, step);
+    k_expand<<<AZ_EXPAND_WAVE ? G : (G + AZ_EXPAND_GPW - 1) / AZ_EXPAND_GPW, 64, 0, st>>>(E, step);
     if (ev) (void)hipEventRecord(ev[2], st);
     int rc = eval_step(s, step, ev);
     if (rc) return rc;

@@ -538,7 +538,7 @@ __device__ __forceinline__ void heads_group(const char* __restrict__ xb, float* 
                 int* sl = reinterpret_cast<int*>(stat + bb * (2 * NW + 4) + 2 * NW + 1);
                 sl[0] = -1;
                 if (b0 + bb >= nb) continue;
-                const int row = row0 + b0 + bb;
+                const int row = vgpr_index(row0 + b0 + bb);
                 const int game = so.row_game[row], node = so.row_node[row];
                 const Node nd = so.nodes[(size_t)game * so.NMAX + node];
                 const int r = atomicAdd(&so.ctr->log_count, 1);
@@ -557,7 +557,7 @@ __device__ __forceinline__ void heads_group(const char* __restrict__ xb, float* 
         float sum = 0.0f;
         for (int i = 0; i < NW; i++) sum += st[NW + i];
         const float value = st[2 * NW];
-        const int row = row0 + b0 + bb;
+        const int row = vgpr_index(row0 + b0 + bb);
         const float* lb = lg + bb * 4096;
         if constexpr (!SEARCH) {
             float* pr = pol_out + (size_t)row * 4096;
@@ -608,7 +608,7 @@ tower_kernel(const __bf16* __restrict__ planes, TowerArgs ta, const int* __restr
     // chunk-group split + per-wave done flags (no barrier between residual convs): F = 256 only
     constexpr int NSP = (AZ_TOWER_FLAGS && F == 256 && WB == 1) ? 2 : 1;
     __shared__ __attribute__((aligned(16))) uint4 lds[XSZ + HSZ + ZN + 6];
-    const int count = count_ptr ? min(*count_ptr, rows) : rows;
+    const int count = count_ptr ? min(load_fresh(count_ptr), rows) : rows;
     const int row0 = blockIdx.x * BPB;
     if (row0 >= count) return;
     const int nb = min(BPB, count - row0);
@@ -654,7 +654,7 @@ tower_kernel(const __bf16* __restrict__ planes, TowerArgs ta, const int* __restr
         for (int rowi = tid; rowi < BPB * 64; rowi += NT) {
             uint4 q[4] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
             if (rowi < nb * 64) {
-                const int row = row0 + (rowi >> 6), sq = rowi & 63;
+                const int row = vgpr_index(row0 + (rowi >> 6)), sq = rowi & 63;
                 const azc::Pos p = so.npos[(size_t)so.row_game[row] * so.NMAX + so.row_node[row]];
                 __bf16 v[32];
 #pragma unroll
@@ -882,7 +882,7 @@ tower32_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __rest
     constexpr int HSZ = ((XSZ > HSZ0 ? XSZ : HSZ0) + 15) / 16 * 16;
     static_assert(BPB * 64 * RSI <= HSZ, "input planes must fit in h");
     __shared__ __attribute__((aligned(16))) uint4 lds[XSZ + HSZ + ZN];
-    const int count = count_ptr ? min(*count_ptr, rows) : rows;
+    const int count = count_ptr ? min(load_fresh(count_ptr), rows) : rows;
     const int row0 = blockIdx.x * BPB;
     if (row0 >= count) return;
     const int nb = min(BPB, count - row0);
@@ -908,7 +908,7 @@ tower32_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __rest
 #pragma unroll
             for (int c = 0; c < 32; c++) v[c] = 0.0f;
             if (rowi < nb * 64) {
-                const int row = row0 + (rowi >> 6), sq = rowi & 63;
+                const int row = vgpr_index(row0 + (rowi >> 6)), sq = rowi & 63;
                 const azc::Pos p = so.npos[(size_t)so.row_game[row] * so.NMAX + so.row_node[row]];
 #pragma unroll
                 for (int c = 0; c < 19; c++) v[c] = azc::plane_value(p, c, sq);

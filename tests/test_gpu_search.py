@@ -35,9 +35,13 @@ def histories(n, seed, max_len=30):
     return out
 
 
+@pytest.mark.parametrize("fused", ["1", "0"])
 @pytest.mark.parametrize("noise", [False, True])
 @pytest.mark.parametrize("sims", [16, 100])
-def test_search_synthetic_bit_exact(require_gpu, noise, sims):
+def test_search_synthetic_bit_exact(require_gpu, noise, sims, fused, monkeypatch):
+    """fused = 1: k_step (backup + select + expand in one launch); 0: separate k_select /
+    k_expand / k_backup launches."""
+    monkeypatch.setenv("AZ_FUSED_STEPS", fused)
     hs = histories(12, sims + noise)
     s = A.BatchedSearch(None, games=len(hs), sims=sims, noise=noise, seed=11)
     s.set_roots(hs, apply_noise=noise)
