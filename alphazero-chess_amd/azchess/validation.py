@@ -88,11 +88,13 @@ def evaluate(player_1, player_2, games=EVALUATION_GAMES, sims=NUM_SIMULATIONS,
     states = [GameState() for _ in range(G)]
     hist = [[] for _ in range(G)]
     result = [None] * G                           # White's result: 1, 0, -1
-    half = (G + 1) // 2
+    # a player moves in at most half of the games at once, or in all of them when it plays both
+    # colours (player_1 is player_2)
+    slots = G if player_1 is player_2 else (G + 1) // 2
     searches = {}
     for p in (player_1, player_2):
         if p.kind == "mcts" and id(p) not in searches:
-            searches[id(p)] = BatchedSearch(p.model, games=half, device=device, sims=sims, noise=False,
+            searches[id(p)] = BatchedSearch(p.model, games=slots, device=device, sims=sims, noise=False,
                                             cache_capacity=0)
     num_inferences, rows = 0, 0
     for ply in range(max_plies):
@@ -116,7 +118,7 @@ def evaluate(player_1, player_2, games=EVALUATION_GAMES, sims=NUM_SIMULATIONS,
                 continue
             if p.kind == "mcts":
                 s = searches[id(p)]
-                roots = [hist[g] for g in gs] + [hist[gs[0]]] * (half - len(gs))   # pad with a live root
+                roots = [hist[g] for g in gs] + [hist[gs[0]]] * (slots - len(gs))   # pad with a live root
                 e0 = s.stats()["evals"]
                 s.set_roots(roots, apply_noise=False)
                 imp, _, _ = s.run()

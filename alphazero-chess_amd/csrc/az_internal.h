@@ -116,6 +116,7 @@ struct Engine {
     float* cached_value;                   // [G] value of a cache-served leaf
     unsigned long long* g_sims;            // [G] simulations backed up (summed at readout)
     unsigned long long* g_sel_bytes;       // [G] algorithmic bytes read by k_select
+    unsigned long long* trace;             // [G][8] s_memtime phase stamps of k_step (AZ_STEP_TRACE builds only)
     // evaluation log
     int log_cap, log_prior_cap;
     unsigned long long* log_key; float* log_value; int* log_off; int* log_n; int* log_idx; float* log_prior;

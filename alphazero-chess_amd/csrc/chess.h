@@ -36,6 +36,14 @@ struct Pos {                       // == az_pos (include/az.h), 80 bytes
     uint64_t rep_key;
 };
 
+AZ_HD uint64_t side_bb(const Pos& p, int color) { return color ? p.bb[BLACK_BB] : p.bb[WHITE_BB]; }
+AZ_HD uint64_t role_bb(const Pos& p, int role) {
+    uint64_t r = p.bb[0];
+#pragma unroll
+    for (int i = 1; i < 6; i++) r = role == i ? p.bb[i] : r;
+    return r;
+}
+
 constexpr uint64_t FILE_A = 0x0101010101010101ULL;
 constexpr uint64_t FILE_H = FILE_A << 7;
 constexpr uint64_t NOT_A = ~FILE_A;
@@ -50,6 +58,11 @@ constexpr uint64_t ALL = ~0ULL;
 
 AZ_HD int ctz64(uint64_t b) { return __builtin_ctzll(b); }
 AZ_HD int popc64(uint64_t b) { return __builtin_popcountll(b); }
+// bitboard accessors with a run-time colour / role: selects over static indices, so a Pos in
+// registers is never indexed dynamically (which would move it to scratch memory on the GPU)
+struct Pos;
+AZ_HD uint64_t side_bb(const Pos& p, int color);
+AZ_HD uint64_t role_bb(const Pos& p, int role);
 
 AZ_HD uint64_t splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ULL;
@@ -108,9 +121,11 @@ AZ_HD uint64_t pawn_att(int color, uint64_t b) {
 }
 
 AZ_HD int piece_role_at(const Pos& p, int sq) {
-    uint64_t m = 1ULL << sq;
-    for (int r = 0; r < 6; r++) if (p.bb[r] & m) return r;
-    return -1;
+    const uint64_t m = 1ULL << sq;
+    int role = -1;
+#pragma unroll
+    for (int r = 5; r >= 0; r--) role = (p.bb[r] & m) ? r : role;
+    return role;
 }
 
 // chess.rs:73-116 move_to_index (to = rook square for castling, shakmaty Move::to())
@@ -136,10 +151,10 @@ AZ_HD int move_index(int from, int to, int turn) {
 
 // plane -> (df, dr) in the mover's frame (chess.rs:131-150)
 AZ_HD void plane_delta(int plane, int& df, int& dr) {
-    if (plane < 8) {
-        const int kdf[8] = {1, 2, 2, 1, -1, -2, -2, -1};
-        const int kdr[8] = {2, 1, -1, -2, -2, -1, 1, 2};
-        df = kdf[plane]; dr = kdr[plane];
+    if (plane < 8) {                 // (1,2) (2,1) (2,-1) (1,-2) (-1,-2) (-2,-1) (-2,1) (-1,2), as selects
+        const int a = (plane == 0 || plane == 3 || plane == 4 || plane == 7) ? 1 : 2;
+        df = plane < 4 ? a : -a;
+        dr = (plane == 0 || plane == 7) ? 2 : (plane == 1 || plane == 6) ? 1 : (plane == 2 || plane == 5) ? -1 : -2;
     } else if (plane < 15) { df = 0; dr = plane - 7; }
     else if (plane < 22) { df = plane - 14; dr = plane - 14; }
     else if (plane < 29) { df = plane - 21; dr = 0; }
@@ -151,7 +166,7 @@ AZ_HD void plane_delta(int plane, int& df, int& dr) {
 }
 
 AZ_HD bool insufficient_side(const Pos& p, int c) {
-    uint64_t ours = p.bb[WHITE_BB + c], theirs = p.bb[WHITE_BB + (c ^ 1)];
+    uint64_t ours = side_bb(p, c), theirs = side_bb(p, c ^ 1);
     if (ours & (p.bb[PAWN] | p.bb[ROOK] | p.bb[QUEEN])) return false;
     if (ours & p.bb[KNIGHT]) return popc64(ours) <= 2 && (theirs & ~p.bb[KING] & ~p.bb[QUEEN]) == 0;
     if (ours & p.bb[BISHOP]) {
@@ -165,7 +180,7 @@ AZ_HD bool insufficient_material(const Pos& p) { return insufficient_side(p, 0) 
 // pseudo-legal ep: a side-to-move pawn attacks the skipped square (shakmaty)
 AZ_HD uint8_t pseudo_ep(const Pos& p, int ep_sq) {
     if (ep_sq >= 64) return 64;
-    uint64_t ours = p.bb[PAWN] & p.bb[WHITE_BB + p.turn];
+    uint64_t ours = p.bb[PAWN] & side_bb(p, p.turn);
     return (pawn_att(p.turn ^ 1, 1ULL << ep_sq) & ours) ? (uint8_t)ep_sq : (uint8_t)64;
 }
 
@@ -195,7 +210,7 @@ AZ_HD bool chess_eq(const Pos& a, const Pos& b) {
 // Returns the number of distinct indices; *in_check, *legal_ep set.
 template <class Sink> AZ_HD int gen_legal(const Pos& p, Sink& sink, bool* in_check, bool* legal_ep) {
     const int us = p.turn, them = us ^ 1;
-    const uint64_t our = p.bb[WHITE_BB + us], their = p.bb[WHITE_BB + them];
+    const uint64_t our = side_bb(p, us), their = side_bb(p, them);
     const uint64_t occ = our | their, empty = ~occ;
     const uint64_t kbb = p.bb[KING] & our;
     const int ksq = ctz64(kbb);
@@ -293,7 +308,7 @@ template <class Sink> AZ_HD int gen_legal(const Pos& p, Sink& sink, bool* in_che
         }
 #pragma unroll
         for (int role = BISHOP; role <= QUEEN; role++) {
-            fr = p.bb[role] & our;
+            fr = role_bb(p, role) & our;
             while (fr) {
                 const int from = ctz64(fr); fr &= fr - 1;
                 const uint64_t sb = 1ULL << from;
@@ -340,7 +355,7 @@ AZ_HD Pos play_index(const Pos& p, int idx) {
     Pos c = p;
     const uint64_t fb = 1ULL << from, tb = 1ULL << to;
     const int role = piece_role_at(p, from);
-    const uint64_t our = p.bb[WHITE_BB + us];
+    const uint64_t our = side_bb(p, us);
     const int home = us == 0 ? 0 : 56;
     bool is_castle = false;
     if (role == KING) {
@@ -350,28 +365,35 @@ AZ_HD Pos play_index(const Pos& p, int idx) {
     }
     bool capture = false;
     int new_ep = 64;
+    // colour / role updates as masks applied to every bitboard (static indices only)
+    uint64_t xor_us = 0, clr_them = 0, clr_all = 0;
+    uint64_t role_clr[6] = {0, 0, 0, 0, 0, 0}, role_set[6] = {0, 0, 0, 0, 0, 0};
     if (is_castle) {
         const bool ks = to > from;
         const int kto = home + (ks ? 6 : 2), rto = home + (ks ? 5 : 3);
         c.bb[KING] ^= fb | (1ULL << kto);
         c.bb[ROOK] ^= tb | (1ULL << rto);
-        c.bb[WHITE_BB + us] ^= fb | tb | (1ULL << kto) | (1ULL << rto);
+        xor_us = fb | tb | (1ULL << kto) | (1ULL << rto);
         c.castling &= us == 0 ? ~3 : ~12;
     } else {
-        if (p.bb[WHITE_BB + them] & tb) {             // capture
+        if (side_bb(p, them) & tb) {                  // capture
             capture = true;
-            for (int r = 0; r < 6; r++) c.bb[r] &= ~tb;
-            c.bb[WHITE_BB + them] &= ~tb;
+            clr_all = tb;
+            clr_them = tb;
         } else if (role == PAWN && df != 0) {          // en passant
             capture = true;
             const uint64_t cb = 1ULL << (us == 0 ? to - 8 : to + 8);
-            c.bb[PAWN] &= ~cb;
-            c.bb[WHITE_BB + them] &= ~cb;
+            role_clr[PAWN] = cb;
+            clr_them = cb;
         }
-        c.bb[role] &= ~fb;
         const bool promo = role == PAWN && (tb & BACKRANKS);
-        c.bb[promo ? QUEEN : role] |= tb;
-        c.bb[WHITE_BB + us] ^= fb | tb;
+        const int placed = promo ? QUEEN : role;
+#pragma unroll
+        for (int r = 0; r < 6; r++) {
+            if (r == role) role_clr[r] |= fb;
+            if (r == placed) role_set[r] |= tb;
+        }
+        xor_us = fb | tb;
         if (role == KING) c.castling &= us == 0 ? ~3 : ~12;
         if (from == 7 || to == 7) c.castling &= ~1;
         if (from == 0 || to == 0) c.castling &= ~2;
@@ -379,6 +401,10 @@ AZ_HD Pos play_index(const Pos& p, int idx) {
         if (from == 56 || to == 56) c.castling &= ~8;
         if (role == PAWN && (dr == 2 || dr == -2)) new_ep = (from + to) >> 1;
     }
+#pragma unroll
+    for (int r = 0; r < 6; r++) c.bb[r] = ((c.bb[r] & ~clr_all) & ~role_clr[r]) | role_set[r];
+    c.bb[WHITE_BB] = (c.bb[WHITE_BB] ^ (us == 0 ? xor_us : 0)) & ~(us == 0 ? 0 : clr_them);
+    c.bb[BLACK_BB] = (c.bb[BLACK_BB] ^ (us == 1 ? xor_us : 0)) & ~(us == 1 ? 0 : clr_them);
     c.turn = (uint8_t)them;
     c.halfmoves = (role == PAWN || capture) ? 0 : (uint16_t)(p.halfmoves + 1);
     if (us == 1) c.fullmoves = (uint16_t)(p.fullmoves + 1);
@@ -430,7 +456,7 @@ AZ_HD float plane_value(const Pos& p, int plane, int sq /* rank'*8+file */) {
     const uint64_t m = 1ULL << real;
     if (plane < 12) {
         const int color = plane < 6 ? us : us ^ 1;
-        return (p.bb[plane % 6] & p.bb[WHITE_BB + color] & m) ? 1.0f : 0.0f;
+        return (role_bb(p, plane % 6) & side_bb(p, color) & m) ? 1.0f : 0.0f;
     }
     switch (plane) {
         case 12: return (p.castling & (us == 0 ? 1 : 4)) ? 1.0f : 0.0f;

@@ -23,6 +23,7 @@
 // other node (traverse_new, tree.rs:239-256), then applies Dirichlet noise
 // (tree.rs:272-289).  Nothing crosses PCIe inside a move.
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -42,6 +43,51 @@ __device__ __forceinline__ Edge* game_edges(const Engine& E, int g) { return E.e
 __device__ __forceinline__ azc::Pos* game_npos(const Engine& E, int g) { return E.npos + (size_t)g * E.NMAX; }
 
 __device__ __forceinline__ int* step_rows(const Engine& E, int step) { return &E.ctr->batch_count[step & 1]; }
+
+// ------------------------------------------------------------------ wave primitives (DPP / ballot)
+// Cross-lane reductions without LDS: __shfl_* lower to ds_bpermute (~100+ cycles a step on a lone
+// wave), DPP moves run at VALU latency.  gfx9 row_bcast15/31 carry row maxima across the 4 rows.
+template <int CTRL, int ROWMASK = 0xF>
+__device__ __forceinline__ float dpp_f32(float old, float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old),
+                                                                 __builtin_bit_cast(int, v), CTRL, ROWMASK, 0xF, false));
+}
+template <int CTRL, int ROWMASK = 0xF>
+__device__ __forceinline__ int dpp_i32(int old, int v) {
+    return __builtin_amdgcn_update_dpp(old, v, CTRL, ROWMASK, 0xF, false);
+}
+// maximum over the wave of a non-NaN float (all lanes active); result wave-uniform
+__device__ __forceinline__ float wave_max_f32(float v) {
+    v = fmaxf(v, dpp_f32<0xB1>(v, v));         // quad_perm [1,0,3,2]
+    v = fmaxf(v, dpp_f32<0x4E>(v, v));         // quad_perm [2,3,0,1]
+    v = fmaxf(v, dpp_f32<0x141>(v, v));        // row_half_mirror
+    v = fmaxf(v, dpp_f32<0x140>(v, v));        // row_mirror: every lane holds its row's max
+    v = fmaxf(v, dpp_f32<0x142, 0xA>(v, v));   // row_bcast:15 -> rows 1, 3
+    v = fmaxf(v, dpp_f32<0x143, 0xC>(v, v));   // row_bcast:31 -> rows 2, 3: lane 63 = wave max
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+__device__ __forceinline__ int wave_min_i32(int v) {
+    v = min(v, dpp_i32<0xB1>(v, v));
+    v = min(v, dpp_i32<0x4E>(v, v));
+    v = min(v, dpp_i32<0x141>(v, v));
+    v = min(v, dpp_i32<0x140>(v, v));
+    v = min(v, dpp_i32<0x142, 0xA>(v, v));
+    v = min(v, dpp_i32<0x143, 0xC>(v, v));
+    return __builtin_amdgcn_readlane(v, 63);
+}
+// exclusive prefix sum over the wave of a small count (0..31) by its bits: one ballot and one
+// mbcnt per bit; *total = the wave sum (uniform)
+__device__ __forceinline__ int wave_excl_small(int cnt, int* total) {
+    int pre = 0, tot = 0;
+#pragma unroll
+    for (int b = 0; b < 5; b++) {
+        const unsigned long long m = __ballot((cnt >> b) & 1);
+        pre += (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u)) << b;
+        tot += __popcll(m) << b;
+    }
+    *total = tot;
+    return pre;
+}
 
 // ------------------------------------------------------------------ select
 // one wavefront walks game g (active) from the root to a leaf
@@ -66,11 +112,13 @@ __device__ __forceinline__ void select_game(const Engine& E, int g, int lane) {
             const float v = q + u;
             if (v > best) { best = v; bpos = e; }
         }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            const float ob = __shfl_xor(best, o, 64);
-            const int op = __shfl_xor(bpos, o, 64);
-            if (ob > best || (ob == best && op < bpos)) { best = ob; bpos = op; }
+        // wave argmax, first maximum in `moves` order: the wave max, then the lowest edge index
+        // among the lanes holding it (lane order = edge order while nedges <= 64)
+        {
+            const float wmax = wave_max_f32(best);
+            const unsigned long long hit = __ballot(best == wmax);
+            if (nd.nedges <= 64) bpos = __builtin_amdgcn_readlane(bpos, (int)__builtin_ctzll(hit));
+            else bpos = wave_min_i32(best == wmax ? bpos : 0x7fffffff);
         }
         bytes += 16ull * nd.nedges + 16ull + 4ull;
         // no edge beat -inf: every value is NaN (a diverged network).  The reference keeps its
@@ -240,20 +288,27 @@ __device__ __forceinline__ int expand_leaf(const Engine& E, int g, int* nid_out)
 #ifndef AZ_EXPAND_WAVE
 #define AZ_EXPAND_WAVE 1   // 0: the one-lane serial expansion (A/B)
 #endif
-__device__ __forceinline__ int wave_scan_incl(int v, int lane) {
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int t = __shfl_up(v, o, 64);
-        if (lane >= o) v += t;
-    }
-    return v;
+// move_to_index (chess.rs:73-116, azc::move_index) as selects only: the lanes of a wave index
+// different moves at once, and the if-chain form diverges into up to 12 serial paths
+__device__ __forceinline__ int move_index_bf(int from, int to, int turn) {
+    const int file = from & 7, rank = turn ? 7 - (from >> 3) : (from >> 3);
+    const int dfile = to & 7, drank = turn ? 7 - (to >> 3) : (to >> 3);
+    const int df = dfile - file, dr = drank - rank;
+    const int adf = df < 0 ? -df : df;
+    const int kn = df > 0 ? (dr > 0 ? (adf == 1 ? 0 : 1) : (adf == 2 ? 2 : 3))
+                          : (dr < 0 ? (adf == 1 ? 4 : 5) : (adf == 2 ? 6 : 7));
+    const int qp = df == 0 ? (dr > 0 ? 7 + dr : 35 - dr)
+                 : dr == 0 ? (df > 0 ? 21 + df : 49 - df)
+                 : df > 0 ? (dr > 0 ? 14 + dr : 28 + df) : (dr < 0 ? 42 - dr : 56 - df);
+    const int plane = df != 0 && dr != 0 && adf + (dr < 0 ? -dr : dr) == 3 ? kn : qp;
+    return plane * 64 + rank * 8 + file;
 }
 
 __device__ __forceinline__ int gen_legal_wave(const azc::Pos& p, Edge* __restrict__ out, int lane, bool* in_check,
-                                           bool* legal_ep) {
+                                           bool* legal_ep, unsigned long long* tr = nullptr) {
     using namespace azc;
     const int us = p.turn, them = us ^ 1;
-    const uint64_t our = p.bb[WHITE_BB + us], their = p.bb[WHITE_BB + them];
+    const uint64_t our = side_bb(p, us), their = side_bb(p, them);
     const uint64_t occ = our | their, empty = ~occ;
     const uint64_t kbb = p.bb[KING] & our;
     const int ksq = ctz64(kbb);
@@ -285,81 +340,111 @@ __device__ __forceinline__ int gen_legal_wave(const azc::Pos& p, Edge* __restric
         return r;
     };
     const uint64_t sb = 1ULL << lane;
-    int base = 0;
-    // one generation group: this lane's targets t (ascending to-squares) from square `from`
-    auto emit = [&](uint64_t t, int from, int flag) {
-        const int cnt = popc64(t);
-        if (__ballot(cnt != 0) == 0) return;
-        const int incl = wave_scan_incl(cnt, lane);
-        int pos = base + incl - cnt;
-        while (t) {
-            const int to = ctz64(t);
-            t &= t - 1;
-            Edge e;
-            e.P = 0.0f; e.W = 0.0f; e.N = 0; e.idx = (uint16_t)(move_index(from, to, us) | flag); e.child = CHILD_NONE;
-            out[pos++] = e;
-        }
-        base += __shfl(incl, 63, 64);
-    };
+    if (tr && lane == 0) tr[8] = __builtin_amdgcn_s_memtime();
     *in_check = checkers != 0;
-    *legal_ep = false;
-    if (p.ep < 64) {                                   // en passant first, full attack test
+    const int nchk = popc64(checkers);
+    // double check: only the king moves (and ep, whose attack test rejects it) -- empty target
+    const uint64_t target = nchk == 0 ? ~our : (nchk == 1 ? checkmask : 0);
+    const uint64_t ourP = p.bb[PAWN] & our;
+    const uint64_t seventh = ourP & (us == 0 ? (0xFFULL << 48) : (0xFFULL << 8));
+    const uint64_t single = (us == 0 ? (ourP << 8) : (ourP >> 8)) & empty;
+    const uint64_t dbl = (us == 0 ? (single << 8) & (0xFFULL << 24) : (single >> 8) & (0xFFULL << 32)) & empty;
+    const int home = us == 0 ? 0 : 56;
+    // Generation groups in shakmaty order -- no check: ep, pawn captures, capture promotions,
+    // pushes, push promotions, double pushes, N, B, R, Q, king, O-O, O-O-O; in check: ep, king,
+    // then the non-king groups on the check mask.  Every lane is in at most one "main" group (the
+    // piece on its square, or the pawn push landing on it) and computes its targets once; a move's
+    // position is the count of all moves in earlier groups plus those of lower lanes in its own
+    // group, from one ballot per group and one per bit of the count (no per-group passes).  The ep
+    // captures (pawn lanes) come first, O-O / O-O-O (the king's lane) after the king moves.
+    enum { G_CAP = 1, G_CPROMO, G_PUSH, G_PPROMO, G_DBL, G_N, G_B, G_R, G_Q, G_K, G_NONE };
+    int grp = G_NONE, from = lane, flag = 0;
+    uint64_t t = 0;
+    const int role = piece_role_at(p, lane);
+    if ((our >> lane) & 1) {
+        const uint64_t allow = allowed(lane);
+        if (role == PAWN) {
+            grp = ((seventh >> lane) & 1) ? G_CPROMO : G_CAP;
+            flag = grp == G_CPROMO ? PROMO_FLAG : 0;
+            t = pawn_att(us, sb) & their & target & allow;
+        } else if (role == KNIGHT) {
+            grp = G_N;
+            t = ((pinned >> lane) & 1) ? 0 : knight_att(sb) & target;
+        } else if (role == KING) {
+            grp = G_K;
+            t = king_att(kbb) & ~our & ~attacked;
+        } else {                                       // B, R, Q
+            grp = G_B + (role - BISHOP);
+            const uint64_t a = (role != ROOK ? bishop_att(sb, empty) : 0) | (role != BISHOP ? rook_att(sb, empty) : 0);
+            t = a & target & allow;
+        }
+    } else if ((((single | dbl) & target) >> lane) & 1) {   // lane = a push's to-square
+        const bool two = (dbl >> lane) & 1;
+        from = us == 0 ? lane - (two ? 16 : 8) : lane + (two ? 16 : 8);
+        grp = two ? G_DBL : (((BACKRANKS >> lane) & 1) ? G_PPROMO : G_PUSH);
+        flag = grp == G_PPROMO ? PROMO_FLAG : 0;
+        if ((allowed(from & 63) >> lane) & 1) t = sb;
+    }
+    // en passant (first in both orders), full attack test
+    uint64_t ep_to = 0;
+    if (p.ep < 64) {
         const uint64_t epbb = 1ULL << p.ep;
-        const int capsq = us == 0 ? p.ep - 8 : p.ep + 8;
-        const uint64_t capbb = 1ULL << capsq;
-        const uint64_t fr = p.bb[PAWN] & our & pawn_att(them, epbb);
-        uint64_t t = 0;
-        if ((fr >> lane) & 1) {
+        const uint64_t capbb = 1ULL << (us == 0 ? p.ep - 8 : p.ep + 8);
+        if (((ourP & pawn_att(them, epbb)) >> lane) & 1) {
             const uint64_t occ2 = (occ ^ sb ^ capbb) | epbb;
             const uint64_t att2 = (rook_att(kbb, ~occ2) & tR) | (bishop_att(kbb, ~occ2) & tB) |
                                   (knight_att(kbb) & tN) | (pawn_att(us, kbb) & tP & ~capbb);
-            if (!att2) t = epbb;
+            if (!att2) ep_to = epbb;
         }
-        *legal_ep = __ballot(t != 0) != 0;
-        emit(t, lane, 0);
     }
-    const int nchk = popc64(checkers);
-    auto non_king = [&](uint64_t target) {
-        const uint64_t ourP = p.bb[PAWN] & our;
-        const uint64_t seventh = ourP & (us == 0 ? (0xFFULL << 48) : (0xFFULL << 8));
-        const uint64_t patt = pawn_att(us, sb) & their & target;
-        emit(((ourP & ~seventh) >> lane) & 1 ? patt & allowed(lane) : 0, lane, 0);          // captures
-        emit((seventh >> lane) & 1 ? patt & allowed(lane) : 0, lane, PROMO_FLAG);          // capture promotions
-        const uint64_t single = (us == 0 ? (ourP << 8) : (ourP >> 8)) & empty;
-        const uint64_t dbl = (us == 0 ? (single << 8) & (0xFFULL << 24) : (single >> 8) & (0xFFULL << 32)) & empty;
-        const int f1 = us == 0 ? lane - 8 : lane + 8, f2 = us == 0 ? lane - 16 : lane + 16;   // pushes: lane = to
-        const bool s1 = ((single & target) >> lane) & 1, s2 = ((dbl & target) >> lane) & 1;
-        const bool ok1 = s1 && ((allowed(f1 & 63) >> lane) & 1);
-        const bool ok2 = s2 && ((allowed(f2 & 63) >> lane) & 1);
-        emit(ok1 && !((BACKRANKS >> lane) & 1) ? sb : 0, f1, 0);                           // single pushes
-        emit(ok1 && ((BACKRANKS >> lane) & 1) ? sb : 0, f1, PROMO_FLAG);                   // push promotions
-        emit(ok2 ? sb : 0, f2, 0);                                                          // double pushes
-        emit(((p.bb[KNIGHT] & our & ~pinned) >> lane) & 1 ? knight_att(sb) & target : 0, lane, 0);
-        emit(((p.bb[BISHOP] & our) >> lane) & 1 ? bishop_att(sb, empty) & target & allowed(lane) : 0, lane, 0);
-        emit(((p.bb[ROOK] & our) >> lane) & 1 ? rook_att(sb, empty) & target & allowed(lane) : 0, lane, 0);
-        emit(((p.bb[QUEEN] & our) >> lane) & 1
-                 ? (bishop_att(sb, empty) | rook_att(sb, empty)) & target & allowed(lane) : 0, lane, 0);
+    const unsigned long long ep_mask = __ballot(ep_to != 0);
+    *legal_ep = ep_mask != 0;
+    const int n_ep = __popcll(ep_mask);
+    // group order: rank of this lane's group; moves of all lanes whose group ranks lower come first
+    const int cnt = t ? popc64(t) : 0;
+    const int rank = nchk == 0 ? grp : (grp == G_K ? G_CAP : (grp < G_K ? grp + 1 : grp));
+    unsigned long long before = 0, same = 0;         // lanes with a lower-ranked / the same group
+#pragma unroll
+    for (int g = G_CAP; g <= G_K; g++) {
+        const int rg = nchk == 0 ? g : (g == G_K ? G_CAP : g + 1);
+        const unsigned long long m = __ballot(grp == g && cnt > 0);
+        before |= rg < rank ? m : 0ull;
+        same = rg == rank ? m : same;
+    }
+    const unsigned long long below = same & ((1ull << lane) - 1ull);
+    int mpos = n_ep, total = n_ep;
+#pragma unroll
+    for (int b = 0; b < 5; b++) {                     // counts <= 27: five bits
+        const unsigned long long mb = __ballot((cnt >> b) & 1);
+        mpos += (__popcll(mb & before) + __popcll(mb & below)) << b;
+        total += __popcll(mb) << b;
+    }
+    if (tr && lane == 0) tr[9] = __builtin_amdgcn_s_memtime();
+    auto put = [&](int pos, int f, int to, int fl) {
+        Edge e;
+        e.P = 0.0f; e.W = 0.0f; e.N = 0; e.idx = (uint16_t)(move_index_bf(f, to, us) | fl); e.child = CHILD_NONE;
+        out[pos] = e;
     };
-    const uint64_t kt = lane == ksq ? king_att(kbb) & ~our & ~attacked : 0;
-    if (nchk == 0) {
-        non_king(~our);
-        emit(kt, ksq, 0);
-        const int home = us == 0 ? 0 : 56;
-        const uint8_t kbit = us == 0 ? 1 : 4, qbit = us == 0 ? 2 : 8;
-        const bool oo = (p.castling & kbit) && ksq == home + 4 && ((p.bb[ROOK] & our) >> (home + 7) & 1) &&
-                        !(occ & (3ULL << (home + 5))) && !(attacked & (7ULL << (home + 4)));
-        const bool ooo = (p.castling & qbit) && ksq == home + 4 && ((p.bb[ROOK] & our) >> home & 1) &&
-                         !(occ & (7ULL << (home + 1))) && !(attacked & (7ULL << (home + 2)));
-        emit(lane == 0 && oo ? 1ULL << (home + 7) : 0, ksq, 0);
-        emit(lane == 0 && ooo ? 1ULL << home : 0, ksq, 0);
-    } else {
-        emit(kt, ksq, 0);
-        if (nchk == 1) non_king(checkmask);
+    if (ep_to) put(__popcll(ep_mask & ((1ull << lane) - 1ull)), lane, p.ep, 0);
+    while (t) {                                        // this lane's main group, ascending to-squares
+        put(mpos++, from, ctz64(t), flag);
+        t &= t - 1;
     }
+    // castling after the king moves (no check only): O-O then O-O-O, from the king's square
+    if (nchk == 0) {
+        const bool oo = (p.castling & (us == 0 ? 1 : 4)) && ksq == home + 4 && ((p.bb[ROOK] & our) >> (home + 7) & 1) &&
+                        !(occ & (3ULL << (home + 5))) && !(attacked & (7ULL << (home + 4)));
+        const bool ooo = (p.castling & (us == 0 ? 2 : 8)) && ksq == home + 4 && ((p.bb[ROOK] & our) >> home & 1) &&
+                         !(occ & (7ULL << (home + 1))) && !(attacked & (7ULL << (home + 2)));
+        if (lane == 0 && oo) put(total, ksq, home + 7, 0);
+        if (lane == 0 && ooo) put(total + (oo ? 1 : 0), ksq, home, 0);
+        total += (oo ? 1 : 0) + (ooo ? 1 : 0);
+    }
+    const int base = total;
     return base;
 }
 
-__device__ __forceinline__ int expand_leaf_wave(const Engine& E, int g, int lane, int* nid_out) {
+__device__ __forceinline__ int expand_leaf_wave(const Engine& E, int g, int lane, int* nid_out, int step = -1) {
     // g is wave-uniform, and a provably uniform index would turn the per-game loads below into
     // scalar (s_load) reads; the leaf records were written by vector stores of another launch
     // (k_select), which the scalar cache does not see -- keep g in a VGPR so they stay vector loads
@@ -378,9 +463,20 @@ __device__ __forceinline__ int expand_leaf_wave(const Engine& E, int g, int lane
     const int hlen = E.hist_len[g];
     const int plen = E.leaf_len[g];
     const int* pn = E.path_node + (size_t)g * E.PMAX;
+    unsigned long long* tr = nullptr;
+#ifdef AZ_STEP_TRACE
+    if (step == AZ_STEP_TRACE) tr = E.trace + (size_t)g * 16;
+    if (tr && lane == 0) tr[10] = __builtin_amdgcn_s_memtime();
+#endif
     azc::Pos c = azc::play_index(pp, idx);
+#ifdef AZ_STEP_TRACE
+    if (tr && lane == 0) tr[11] = __builtin_amdgcn_s_memtime();
+#endif
     bool chk = false, lep = false;
-    const int n = gen_legal_wave(c, edges + ebeg, lane, &chk, &lep);
+    const int n = gen_legal_wave(c, edges + ebeg, lane, &chk, &lep, tr);
+#ifdef AZ_STEP_TRACE
+    if (step == AZ_STEP_TRACE && lane == 0) E.trace[(size_t)g * 16 + 5] = __builtin_amdgcn_s_memtime();
+#endif
     c.flags = lep ? 1 : 0;
     c.rep_key = azc::rep_key_of(c);
     int res = azc::outcome(c, n, chk);
@@ -404,6 +500,9 @@ __device__ __forceinline__ int expand_leaf_wave(const Engine& E, int g, int lane
         if (cnt + 1 >= azc::REPETITIONS || c.halfmoves >= azc::NUM_HALFMOVES || c.fullmoves >= azc::NUM_FULLMOVES)
             res = azc::DRAW;
     }
+#ifdef AZ_STEP_TRACE
+    if (step == AZ_STEP_TRACE && lane == 0) E.trace[(size_t)g * 16 + 6] = __builtin_amdgcn_s_memtime();
+#endif
     if (res != azc::ONGOING) {
         if (lane == 0) {
             edges[eabs].child = res == azc::DRAW ? CHILD_DRAW : CHILD_WIN;
@@ -550,27 +649,39 @@ __global__ void __launch_bounds__(256) k_backup(Engine E, int step) {
 // to its later loads (select) by a workgroup-scope fence.  Rows are allocated with one atomic
 // per workgroup (STEP_WPB games).  bstep's row counter is read and cleared by one thread;
 // step's counter (the other parity) was cleared by the backup of step - 2.
-constexpr int STEP_WPB = 4;     // 256 threads: the expansion needs ~180 VGPRs and its 80-B position stays in registers only up to this size
+#ifndef AZ_STEP_WPB
+#define AZ_STEP_WPB 1      // C2 A/B (profiles/r02_ab_movegen_c2_*.log): 1 wave per workgroup +2.5 % over 4 (no barrier wait on the slowest game)
+#endif
+constexpr int STEP_WPB = AZ_STEP_WPB;   // games (waves) per k_step workgroup
+#ifdef AZ_STEP_TRACE   // experiment: per-wave phase stamps of step AZ_STEP_TRACE (tools/step_trace.py)
+#define ST_STAMP(k) do { if (step == AZ_STEP_TRACE && lane == 0 && g < E.G) E.trace[(size_t)g * 16 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define ST_STAMP(k) do { } while (0)
+#endif
 __global__ void __launch_bounds__(STEP_WPB * 64) k_step(Engine E, int step, int bstep) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int g = blockIdx.x * STEP_WPB + w;
     __shared__ int s_kind[STEP_WPB], s_nid[STEP_WPB], s_base;
+    ST_STAMP(0);
     const bool live = g < E.G && E.active[g];
     if (bstep >= 0) {
         if (blockIdx.x == 0 && threadIdx.x == 0) backup_stats(E, bstep);
         if (live) backup_game(E, g, lane);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     }
+    ST_STAMP(1);
     int kind = X_NONE, nid = -1;
     if (live) {
         select_game(E, g, lane);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        ST_STAMP(2);
 #if AZ_EXPAND_WAVE
-        kind = expand_leaf_wave(E, g, lane, &nid);
+        kind = expand_leaf_wave(E, g, lane, &nid, step);
 #else
         if (lane == 0) kind = expand_leaf(E, g, &nid);
 #endif
     }
+    ST_STAMP(3);
     if (lane == 0) { s_kind[w] = kind; s_nid[w] = nid; }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -592,6 +703,7 @@ __global__ void __launch_bounds__(STEP_WPB * 64) k_step(Engine E, int step, int 
         E.row_node[row] = nid;
         E.leaf_row[g] = row;
     }
+    ST_STAMP(4);
 }
 
 // ------------------------------------------------------------------ roots
@@ -1026,6 +1138,17 @@ int run_sims(az_search* s, int i0 = 0, int i1 = -1) {
     }
     if (pending >= 0) k_backup<<<(s->E.G * 64 + 255) / 256, 256, 0, s->st>>>(s->E, pending);
     AZ_HIP(hipGetLastError());
+#ifdef AZ_STEP_TRACE
+    if (i0 <= AZ_STEP_TRACE && AZ_STEP_TRACE < i1) {
+        std::vector<unsigned long long> h((size_t)s->E.G * 16);
+        AZ_HIP(hipStreamSynchronize(s->st));
+        AZ_HIP(hipMemcpy(h.data(), s->E.trace, h.size() * 8, hipMemcpyDeviceToHost));
+        if (FILE* f = fopen(getenv("AZ_STEP_TRACE_FILE") ? getenv("AZ_STEP_TRACE_FILE") : "step_trace.bin", "ab")) {
+            fwrite(h.data(), 8, h.size(), f);
+            fclose(f);
+        }
+    }
+#endif
     if (tm) {
         AZ_HIP(hipStreamSynchronize(s->st));
         std::vector<int> rows(S);
@@ -1212,6 +1335,9 @@ int az_search_create(az_net* net, const az_search_cfg* cfg, int device, az_searc
     rc |= dalloc(s, &E.batch_hist, S);
     rc |= dalloc(s, &E.cached_value, G);
     rc |= dalloc(s, &E.g_sims, G); rc |= dalloc(s, &E.g_sel_bytes, G);
+#ifdef AZ_STEP_TRACE
+    rc |= dalloc(s, &E.trace, (size_t)G * 16);
+#endif
     E.cache_mask = -1;
     if (cfg->cache_capacity > 0) {
         int slots = 1;

@@ -155,6 +155,11 @@ int ref_search_game(const ref_search_cfg* cfg, const ref_replay* rep, const int3
 int64_t ref_selfplay(const ref_search_cfg* cfg, const ref_replay* rep, int ngames, int max_plies,
                      ref_step* steps, int64_t cap, int64_t* sims_done, int64_t* evals_done);
 
+/* ---- arena / Elo (validation.rs:284-384, ratings.rs:113-144) ---- */
+int  ref_arena_choose(const float* policy, int fullmoves, int num_stochastic_moves, float u);
+void ref_mask_to_legal(const ref_pos* p, float* policy);
+void ref_compute_elos(const float* wm, int n, float base_elo, float* elos);   /* n <= 64 */
+
 #ifdef __cplusplus
 }
 #endif

@@ -420,3 +420,43 @@ int64_t ref_selfplay(const ref_search_cfg* cfg, const ref_replay* rep, int ngame
     if (evals_done) *evals_done = total_evals;
     return any_failed ? -1 : n;
 }
+
+/* ---------------- arena and Elo (validation.rs, ratings.rs) ---------------- */
+
+/* validation.rs:297-308 / 336-346: fullmoves > num_stochastic_moves (strict) -> the last maximal
+ * index (Iterator::max_by over partial_cmp), else WeightedIndex::new(policy).sample() with the
+ * uniform draw u standing in for thread_rng */
+int ref_arena_choose(const float* policy, int fullmoves, int num_stochastic_moves, float u) {
+    if (fullmoves > num_stochastic_moves) return argmax_last(policy);
+    return weighted_index(policy, u);
+}
+
+/* validation.rs:325-335: the base-model player zeroes every index not produced by a legal move */
+void ref_mask_to_legal(const ref_pos* p, float* policy) {
+    ref_move mv[REF_MAX_MOVES];
+    const int n = ref_legal_moves(p, mv);
+    unsigned char legal[REF_ACTION_SPACE];
+    memset(legal, 0, sizeof(legal));
+    for (int i = 0; i < n; i++) legal[ref_move_to_index(mv[i], p->turn)] = 1;
+    for (int i = 0; i < REF_ACTION_SPACE; i++) if (!legal[i]) policy[i] = 0.0f;
+}
+
+/* ratings.rs:113-144: fixed-point Elo fit, f32, LEARNING_RATE 8, 1000 iterations, player 0
+ * pinned at base_elo; expected score 1 / (1 + 10^((prev[j] - prev[i]) / 400)) */
+void ref_compute_elos(const float* wm, int n, float base_elo, float* elos) {
+    float prev[64];
+    for (int i = 0; i < n; i++) elos[i] = base_elo;
+    for (int it = 0; it < 1000; it++) {
+        for (int i = 0; i < n; i++) prev[i] = elos[i];
+        for (int i = 1; i < n; i++) {
+            float actual = 0.0f, expected = 0.0f;
+            for (int j = 0; j < n; j++) {
+                if (i == j) continue;
+                actual += wm[i * n + j];
+                const float diff = prev[j] - prev[i];
+                expected += 1.0f / (1.0f + powf(10.0f, diff / 400.0f));
+            }
+            elos[i] += 8.0f * (actual - expected);
+        }
+    }
+}

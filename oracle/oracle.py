@@ -108,6 +108,9 @@ def lib():
         L.ref_selfplay.argtypes = [P(RefSearchCfg), C.c_void_p, C.c_int, C.c_int, P(RefStep), C.c_int64,
                                    P(C.c_int64), P(C.c_int64)]
         L.ref_selfplay.restype = C.c_int64
+        L.ref_arena_choose.argtypes = [P(C.c_float), C.c_int, C.c_int, C.c_float]
+        L.ref_mask_to_legal.argtypes = [P(RefPos), P(C.c_float)]
+        L.ref_compute_elos.argtypes = [P(C.c_float), C.c_int, C.c_float, P(C.c_float)]
         _lib = L
     return _lib
 
@@ -312,3 +315,26 @@ def selfplay(cfg, ngames, max_plies=0, replay=None, cap=100000):
                         result=s.result, fen_key=s.fen_key,
                         visits={int(s.vis_idx[i]): float(s.vis_n[i]) for i in range(s.nvis)}))
     return out, sims.value, evals.value
+
+
+# ------------------------------------------------------------------ arena / Elo
+def arena_choose(policy, fullmoves, num_stochastic_moves, u):
+    """validation.rs:297-308: strict `>` threshold, last-max argmax, WeightedIndex sample at u."""
+    p = np.ascontiguousarray(policy, np.float32)
+    return lib().ref_arena_choose(_fp(p), int(fullmoves), int(num_stochastic_moves), C.c_float(u))
+
+
+def mask_to_legal(pos, policy):
+    """validation.rs:325-335 on a RefPos: policy with every non-legal index zeroed."""
+    p = np.array(policy, np.float32)
+    lib().ref_mask_to_legal(C.byref(pos), _fp(p))
+    return p
+
+
+def compute_elos(winrate_matrix, base_elo):
+    """ratings.rs:113-144."""
+    wm = np.ascontiguousarray(winrate_matrix, np.float32)
+    n = len(wm)
+    out = np.zeros(n, np.float32)
+    lib().ref_compute_elos(_fp(wm), n, C.c_float(base_elo), _fp(out))
+    return out

@@ -3,6 +3,7 @@ import numpy as np
 import pytest
 
 import azchess as A
+import oracle as O
 from azchess import validation as V
 
 
@@ -43,3 +44,30 @@ def test_stochastic_threshold_is_strict():
     # fullmoves > 15 -> argmax; at exactly 15 the move is still sampled (validation.rs:297)
     assert V.choose(p, 16, 15, 0.95) == 3
     assert V.choose(p, 15, 15, 0.95) == 7
+
+
+def test_compute_elos_matches_oracle():
+    """azchess.compute_elos against the oracle's C restatement of ratings.rs:113-144 (f32, powf)."""
+    rng = np.random.default_rng(7)
+    for n in (2, 3, 5, 8):
+        w = rng.uniform(0.05, 0.95, (n, n)).astype(np.float32)
+        wm = np.triu(w, 1) + np.tril(1.0 - w.T, -1)
+        np.fill_diagonal(wm, 0.5)
+        for base in (0.0, 150.0, 1200.0):
+            a = np.asarray(A.compute_elos(wm, base), np.float64)
+            r = np.asarray(O.compute_elos(wm, base), np.float64)
+            assert np.allclose(a, r, rtol=1e-6, atol=1e-6 * abs(base) + 1e-4), (n, base, a, r)
+
+
+def test_choose_matches_oracle():
+    """The arena's move choice (validation.rs:297-308) against ref_arena_choose on random sparse
+    policies, both sides of the strict threshold, with ties."""
+    rng = np.random.default_rng(11)
+    for trial in range(300):
+        p = np.zeros(4096, np.float32)
+        idx = rng.choice(4096, int(rng.integers(1, 40)), replace=False)
+        p[idx] = rng.integers(1, 6, len(idx)).astype(np.float32)   # small integers: ties are common
+        p /= p.sum()
+        fm = int(rng.integers(10, 20))
+        u = np.float32(rng.random(dtype=np.float32))
+        assert V.choose(p, fm, 15, u) == O.arena_choose(p, fm, 15, u), trial
