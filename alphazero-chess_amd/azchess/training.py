@@ -7,6 +7,7 @@ simulation step evaluates all pending leaves in one batch, with nothing crossing
 until a move's EpisodeSteps are drained.
 """
 import ctypes as C
+import time
 from dataclasses import dataclass
 
 import numpy as np
@@ -236,8 +237,9 @@ def train(iterations, blocks=NUM_RES_BLOCKS, filters=NUM_FILTERS, games=NUM_EPIS
     replay = replay if replay is not None else ReplayBuffer()
     history = []
     for iteration in range(iterations):
+        t0 = time.perf_counter()
         model = trainer.model(dtype)
-        new_unique, plays = 0, 0
+        new_unique, plays, sims_done, games_done = 0, 0, 0, 0
         while True:
             sp = SelfPlay(model, games=games, sims=sims, device=device, continuous=False,
                           seed=seed + 1000003 * rank + 7919 * iteration + 104729 * plays)
@@ -249,8 +251,11 @@ def train(iterations, blocks=NUM_RES_BLOCKS, filters=NUM_FILTERS, games=NUM_EPIS
                 if active == 0:
                     break
             plays += 1
+            sims_done += sp.search.stats()["sims"]
+            games_done += games
             if len(replay) >= min_replay:
                 break
+        t1 = time.perf_counter()
         lr = get_cyclical_lr(iteration)
         pl_sum = vl_sum = 0.0
         for b in range(train_steps):
@@ -258,8 +263,10 @@ def train(iterations, blocks=NUM_RES_BLOCKS, filters=NUM_FILTERS, games=NUM_EPIS
             pl, vl = trainer.step(planes, pol, val, lr)
             pl_sum += pl
             vl_sum += vl
+        t2 = time.perf_counter()
         st = {"iteration": iteration, "replay": len(replay), "new_unique": new_unique, "lr": lr,
-              "policy_loss": pl_sum / max(train_steps, 1), "value_loss": vl_sum / max(train_steps, 1)}
+              "policy_loss": pl_sum / max(train_steps, 1), "value_loss": vl_sum / max(train_steps, 1),
+              "selfplay_s": t1 - t0, "train_s": t2 - t1, "selfplay_games": games_done, "selfplay_sims": sims_done}
         history.append(st)
         if log:
             log(st)
