@@ -11,6 +11,10 @@
 static_assert(sizeof(az_pos) == 80, "az_pos layout");
 static_assert(sizeof(azc::Pos) == sizeof(az_pos), "Pos == az_pos");
 
+#ifndef AZ_WINOGRAD_DEFAULT
+#define AZ_WINOGRAD_DEFAULT 1
+#endif
+
 namespace azi {
 
 void set_error(const std::string& msg);
@@ -128,6 +132,9 @@ struct NetDev {
     std::vector<void*> conv_w;      // swizzled MFMA fragments per conv (1 + 2*blocks)
     std::vector<float*> conv_b;     // folded bias per conv
     std::vector<size_t> conv_bytes; // allocation size of each conv_w (incl. the 8 zero k-steps of prefetch pad)
+    std::vector<void*> wino_w;      // f32 F=256: Winograd-transformed residual conv weights (tower32w_kernel)
+    std::vector<size_t> wino_bytes;
+    bool winograd = AZ_WINOGRAD_DEFAULT != 0;   // tower32w_kernel for f32 F=256 nets (env AZ_WINOGRAD=0/1)
     float* head = nullptr;          // folded head weights (f32)
     void* head_frag = nullptr;      // 1x1 F->40 head conv as bf16 hi/lo MFMA A-fragments (fused tower)
     void* head_frag32 = nullptr;    // the same conv as f32 A-fragments of v_mfma_f32_16x16x4_f32 (f32 fused tower)

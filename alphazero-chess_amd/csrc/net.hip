@@ -430,6 +430,30 @@ std::vector<float> swizzle_f32(const std::vector<float>& wf, int cout, int cin_r
     return o;
 }
 
+// Winograd F(2x2,3x3) weights U = G g G^T (f64, rounded once), fragment-swizzled for the MFMA A
+// operand: [ci/16][xi][co/16][lane][4], lane = co%16 + 16*((ci%16)/4), component ci%4, then 8 zero
+// steps (ring refills past the end); tap = dy*3 + dx as in swizzle_f32
+std::vector<float> winograd_f32(const std::vector<float>& wf, int F) {
+    static const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
+    const int CF = F / 16, NSTEP = (F / 16) * 16;
+    std::vector<float> o((size_t)(NSTEP + 8) * CF * 64 * 4, 0.0f);
+    for (int co = 0; co < F; co++)
+        for (int ci = 0; ci < F; ci++) {
+            const float* g = &wf[((size_t)co * F + ci) * 9];
+            double gg[4][3];
+            for (int a = 0; a < 4; a++)
+                for (int j = 0; j < 3; j++) gg[a][j] = G[a][0] * g[0 * 3 + j] + G[a][1] * g[1 * 3 + j] + G[a][2] * g[2 * 3 + j];
+            for (int a = 0; a < 4; a++)
+                for (int b = 0; b < 4; b++) {
+                    const double u = gg[a][0] * G[b][0] + gg[a][1] * G[b][1] + gg[a][2] * G[b][2];
+                    const int step = (ci / 16) * 16 + a * 4 + b;
+                    const int lane = (co % 16) + 16 * ((ci % 16) / 4);
+                    o[(((size_t)step * CF + co / 16) * 64 + lane) * 4 + ci % 4] = (float)u;
+                }
+        }
+    return o;
+}
+
 }  // namespace
 
 int net_create(const az_net_desc* d, const float* wts, size_t n, int device, NetDev** out) {
@@ -442,6 +466,7 @@ int net_create(const az_net_desc* d, const float* wts, size_t n, int device, Net
     NetDev* net = new NetDev();
     net->blocks = B; net->filters = F; net->dtype = d->dtype; net->device = device;
     if (const char* e = getenv("AZ_FUSED_TOWER")) net->fused = atoi(e) != 0;
+    if (const char* e = getenv("AZ_WINOGRAD")) net->winograd = atoi(e) != 0;
     AZ_HIP(hipStreamCreateWithFlags(&net->stream, hipStreamNonBlocking));
     const float* p = wts;
     auto fold_conv = [&](int cin, const float* w, const float* bias, const float* bn) {
@@ -469,6 +494,14 @@ int net_create(const az_net_desc* d, const float* wts, size_t n, int device, Net
             if (hipMemcpy(dw, s.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) return -1;
         }
         net->conv_bytes.push_back(bytes);
+        if (d->dtype == AZ_DTYPE_F32 && F == 256 && cin == F) {   // Winograd F(2x2,3x3) copy for tower32w_kernel
+            auto u = winograd_f32(wf, F);
+            void* du = nullptr;
+            if (hipMalloc(&du, u.size() * 4) != hipSuccess) return -1;
+            if (hipMemcpy(du, u.data(), u.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return -1;
+            net->wino_w.push_back(du);
+            net->wino_bytes.push_back(u.size() * 4);
+        }
         if (hipMalloc(&db, F * 4) != hipSuccess) return -1;
         if (hipMemcpy(db, bf.data(), F * 4, hipMemcpyHostToDevice) != hipSuccess) return -1;
         net->conv_w.push_back(dw);
@@ -555,6 +588,7 @@ void net_destroy(NetDev* n) {
     if (!n) return;
     (void)hipSetDevice(n->device);
     for (void* w : n->conv_w) (void)hipFree(w);
+    for (void* w : n->wino_w) (void)hipFree(w);
     for (float* b : n->conv_b) (void)hipFree(b);
     (void)hipFree(n->head);
     (void)hipFree(n->head_frag);

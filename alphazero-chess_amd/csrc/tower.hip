@@ -72,6 +72,8 @@ struct TowerArgs {
     const uint4* head_frag;        // 1x1 F->40 head conv as bf16 hi/lo MFMA A-fragments (net.hip)
     const uint4* head_frag32;      // the same conv as f32 A-fragments (f32 tower)
     unsigned wbytes[1 + 2 * 40];   // allocation bytes of each w[i] (buffer-load range check)
+    const uint4* ww[2 * 40];       // f32 Winograd weights of the residual convs (F = 256, tower32w_kernel)
+    unsigned wwbytes[2 * 40];
     int blocks;
 #ifdef AZ_TOWER_TRACE
     unsigned long long* trace;     // experiment only: [grid][TR_SLOTS] s_memrealtime stamps (100 MHz)
@@ -867,6 +869,36 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t t32_rsrc(const uint4* p, unsig
     return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, 0x00020000);
 }
 
+// input planes [row][64][32] f32 -> H (row stride RSI slots): from a planes buffer, or in search
+// mode to_tensor (chess.rs:191-245) from the leaf's packed position, one thread per square
+template <int BPB, int RSI, int NT>
+__device__ __forceinline__ void stage_planes_f32(uint4* H, const float* __restrict__ planes, const SearchOut& so,
+                                                 int row0, int nb, int tid) {
+    if (planes) {
+        const uint4* src = reinterpret_cast<const uint4*>(planes) + (size_t)row0 * 64 * 8;
+        for (int c = tid; c < BPB * 64 * 8; c += NT) {
+            const int rowi = c >> 3, slot = c & 7;
+            H[rowi * RSI + slot] = rowi < nb * 64 ? src[c] : make_uint4(0, 0, 0, 0);
+        }
+    } else {
+        for (int rowi = tid; rowi < BPB * 64; rowi += NT) {
+            float v[32];
+#pragma unroll
+            for (int c = 0; c < 32; c++) v[c] = 0.0f;
+            if (rowi < nb * 64) {
+                const int row = vgpr_index(row0 + (rowi >> 6)), sq = rowi & 63;
+                const azc::Pos p = so.npos[(size_t)so.row_game[row] * so.NMAX + so.row_node[row]];
+#pragma unroll
+                for (int c = 0; c < 19; c++) v[c] = azc::plane_value(p, c, sq);
+            }
+            uint4 q[8];
+            __builtin_memcpy(q, v, sizeof(v));
+#pragma unroll
+            for (int k = 0; k < 8; k++) H[rowi * RSI + k] = q[k];
+        }
+    }
+}
+
 template <int F, bool SEARCH>
 __global__ void __launch_bounds__((F / (16 * Tower32Cfg<F>::NCO)) * Tower32Cfg<F>::WB * 64)
 tower32_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __restrict__ count_ptr, int rows,
@@ -894,31 +926,7 @@ tower32_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __rest
     const int zero_off = (XSZ + HSZ) * 16;
     const char* ldsb = reinterpret_cast<const char*>(lds);
 
-    // input planes [row][64][32] f32 -> H, row stride RSI
-    if (planes) {
-        const uint4* src = reinterpret_cast<const uint4*>(planes) + (size_t)row0 * 64 * 8;
-        for (int c = tid; c < BPB * 64 * 8; c += NT) {
-            const int rowi = c >> 3, slot = c & 7;
-            H[rowi * RSI + slot] = rowi < nb * 64 ? src[c] : make_uint4(0, 0, 0, 0);
-        }
-    } else {
-        // search mode: to_tensor (chess.rs:191-245) from the leaf's packed position, one thread per square
-        for (int rowi = tid; rowi < BPB * 64; rowi += NT) {
-            float v[32];
-#pragma unroll
-            for (int c = 0; c < 32; c++) v[c] = 0.0f;
-            if (rowi < nb * 64) {
-                const int row = vgpr_index(row0 + (rowi >> 6)), sq = rowi & 63;
-                const azc::Pos p = so.npos[(size_t)so.row_game[row] * so.NMAX + so.row_node[row]];
-#pragma unroll
-                for (int c = 0; c < 19; c++) v[c] = azc::plane_value(p, c, sq);
-            }
-            uint4 q[8];
-            __builtin_memcpy(q, v, sizeof(v));
-#pragma unroll
-            for (int k = 0; k < 8; k++) H[rowi * RSI + k] = q[k];
-        }
-    }
+    stage_planes_f32<BPB, RSI, NT>(H, planes, so, row0, nb, tid);
     for (int c = tid; c < ZN; c += NT) lds[XSZ + HSZ + c] = make_uint4(0, 0, 0, 0);
     __syncthreads();
 
@@ -960,6 +968,240 @@ tower32_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __rest
 }
 
 
+// ====================================================================== f32 Winograd tower
+// tower32w_kernel: the same f32 tower with every residual 3x3 conv as Winograd F(2x2, 3x3)
+// (Lavin & Gray): the 8x8 board is 16 output tiles of 2x2 whose 4x4 input patches are
+// transformed V = B^T d B (16 points xi), the weights were transformed on the host
+// U = G g G^T (f64, rounded once to f32), M[xi] = U[xi] V[xi] summed over the input channels is
+// 16 GEMMs of 256 x 16 tiles x 256 on v_mfma_f32_16x16x4_f32 (exact f32 products), and
+// Y = A^T M A.  2.25x fewer MFMAs than the direct conv (16 tiles x 16 points vs 64 squares x 9
+// taps).  Numerics: f32 throughout; the transforms' rounding adds ~1.3x the direct f32 error
+// (numpy check), checked against the oracle within the f32 tolerance.
+// Layout (one board per workgroup, 8 waves of 32 output channels = all 16 points):
+//   ACT [64 squares][66 slots] f32 in LDS -- the layer input, overwritten in place by the output
+//       (the block input x stays in the registers of the wave that owns it, as the residual);
+//   V   2 x [16 xi][8 channel quads][16 tiles][4] f32 = 2 x 32 KB, double-buffered by 32-channel
+//       chunks: chunk c+1 is transformed (one (channel, tile) per thread) while the MFMAs of
+//       chunk c run; one barrier per chunk;
+//   weights [16 ci/16][16 xi][16 co/16][64 lanes][4] f32 per conv, streamed from L2 with a
+//       register ring of WINO_PF (xi, 16-channel) steps.
+#ifndef AZ_WINO_PF
+#define AZ_WINO_PF 2
+#endif
+#ifndef AZ_WINO_LA
+#define AZ_WINO_LA 2
+#endif
+#ifndef AZ_WINO_TLOAD
+#define AZ_WINO_TLOAD 0    // step of a chunk at which the next chunk's patch reads issue
+#endif
+#ifndef AZ_WINO_TSPLIT
+#define AZ_WINO_TSPLIT 8   // steps between the patch reads and their transform + V writes
+#endif
+constexpr int WINO_TLOAD = AZ_WINO_TLOAD, WINO_TSPLIT = AZ_WINO_TSPLIT;
+constexpr int WINO_PF = AZ_WINO_PF;
+constexpr int WINO_LA = AZ_WINO_LA;
+constexpr int WINO_CH = 32;                           // input channels per transform chunk
+constexpr int WINO_VBYTES = 16 * (WINO_CH / 4) * 16 * 16;   // 32 KB per V buffer
+
+template <bool RESID>
+__device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase, int zero_off,
+                                          const __amdgpu_buffer_rsrc_t rW, const float* __restrict__ bias,
+                                          f32x4 (&xres)[2][4], int w, int lane) {
+    constexpr int F = 256, CF = F / 16, RS = F / 4 + 2;
+    constexpr int NCHUNK = F / WINO_CH, SPC = (WINO_CH / 16) * 16;   // 8 chunks x 32 steps
+    constexpr int PF = WINO_PF, LA = WINO_LA;
+    static_assert(SPC % PF == 0 && SPC % LA == 0, "ring slots must be compile-time");
+    const int l16 = lane & 15, h = lane >> 4;
+    const int ty = l16 >> 2, tx = l16 & 3;
+    // transform item of this thread: input channel 4w + h of the chunk, tile l16
+    const int tci4 = (4 * w + h) * 4;
+    const int vwr = w * 256 + l16 * 16 + h * 4;          // + xi * 2048
+    const int vrd = h * 256 + l16 * 16;                  // + xi * 2048 + k * 1024
+    // V[buf] <- B^T d B of chunk c for this thread's item, in two halves: tload issues the 16
+    // patch reads, tstore (WINO_TSPLIT steps later, their latency hidden behind MFMAs) transforms
+    // and writes
+    auto tload = [&](int c, float (&d)[4][4]) {
+        // patch addresses recomputed per chunk from a laundered tile index: hoisted out of the
+        // chunk loop they were 16 loop-invariant registers, and spilled
+        const int tl = vgpr_index(l16);
+        const int pty = 2 * (tl >> 2) - 1, ptx = 2 * (tl & 3) - 1;
+        const int chan = c * WINO_CH * 4 + tci4;
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int py = pty + i, px = ptx + j;
+                const bool ok = (unsigned)py < 8u && (unsigned)px < 8u;
+                d[i][j] = *reinterpret_cast<const float*>(ldsb + (ok ? (py * 8 + px) * RS * 16 : zero_off) + chan);
+            }
+    };
+    auto tstore = [&](int buf, const float (&d)[4][4]) {
+        float t[4][4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            t[0][j] = d[0][j] - d[2][j];
+            t[1][j] = d[1][j] + d[2][j];
+            t[2][j] = d[2][j] - d[1][j];
+            t[3][j] = d[1][j] - d[3][j];
+        }
+        char* vb = ldsb + vbase + buf * WINO_VBYTES + vwr;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const float v0 = t[i][0] - t[i][2], v1 = t[i][1] + t[i][2], v2 = t[i][2] - t[i][1], v3 = t[i][1] - t[i][3];
+            *reinterpret_cast<float*>(vb + (i * 4 + 0) * 2048) = v0;
+            *reinterpret_cast<float*>(vb + (i * 4 + 1) * 2048) = v1;
+            *reinterpret_cast<float*>(vb + (i * 4 + 2) * 2048) = v2;
+            *reinterpret_cast<float*>(vb + (i * 4 + 3) * 2048) = v3;
+        }
+    };
+    // the residual: this wave's outputs of the block input, read before it is overwritten
+    const int co0 = w * 32 + h * 4;
+    auto out_addr = [&](int n, int a, int b) { return ((2 * ty + a) * 8 + 2 * tx + b) * RS * 16 + (co0 + n * 16) * 4; };
+    if constexpr (!RESID) {
+#pragma unroll
+        for (int n = 0; n < 2; n++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) xres[n][q] = *reinterpret_cast<const f32x4*>(ldsb + out_addr(n, q >> 1, q & 1));
+    }
+    f32x4 acc[16][2];
+#pragma unroll
+    for (int x = 0; x < 16; x++) { acc[x][0] = f32x4{0.f, 0.f, 0.f, 0.f}; acc[x][1] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+    // weight ring: steps t (16-channel group kc, xi) = kc * 16 + xi; wave w's two fragments at co/16 = 2w, 2w+1
+    const int voff = (2 * w * 64 + lane) * 16;
+    f32x4 wr[PF][2];
+#pragma unroll
+    for (int i = 0; i < PF; i++)
+#pragma unroll
+        for (int n = 0; n < 2; n++)
+            wr[i][n] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rW, voff + n * 1024 + i * CF * 1024, 0, 0));
+    {
+        float d0[4][4];
+        tload(0, d0);
+        tstore(0, d0);
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int c = 0; c < NCHUNK; c++) {
+        float dn[4][4];
+        const int vb = vbase + (c & 1) * WINO_VBYTES + vrd;
+        const bool more = c + 1 < NCHUNK;
+        f32x4 bq[LA];
+#pragma unroll
+        for (int i = 0; i < LA; i++) bq[i] = *reinterpret_cast<const f32x4*>(ldsb + vb + ((i >> 4) * 1024) + (i & 15) * 2048);
+#pragma unroll
+        for (int st = 0; st < SPC; st++) {
+            const int k = st >> 4, x = st & 15;
+            const f32x4 B = bq[st % LA];
+            if (st + LA < SPC) {
+                const int s2 = st + LA;
+                bq[st % LA] = *reinterpret_cast<const f32x4*>(ldsb + vb + (s2 >> 4) * 1024 + (s2 & 15) * 2048);
+            }
+            f32x4 a[2] = {wr[st % PF][0], wr[st % PF][1]};
+            {
+                const int tn = c * SPC + st + PF;             // past the conv: its zero pad
+#pragma unroll
+                for (int n = 0; n < 2; n++)
+                    wr[st % PF][n] = __builtin_bit_cast(
+                        f32x4, __builtin_amdgcn_raw_buffer_load_b128(rW, voff + n * 1024 + tn * CF * 1024, 0, 0));
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int s4 = 0; s4 < 4; s4++)
+#pragma unroll
+                for (int n = 0; n < 2; n++)
+                    acc[x][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[n][s4], B[s4], acc[x][n], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            (void)k;
+            if (st == WINO_TLOAD && more) tload(c + 1, dn);
+            if (st == WINO_TLOAD + WINO_TSPLIT && more) tstore((c + 1) & 1, dn);
+        }
+        __syncthreads();
+    }
+    // output transform Y = A^T M A per (output fragment n, channel r), + bias (+ residual), ReLU
+#pragma unroll
+    for (int n = 0; n < 2; n++) {
+        const float4 bb = *reinterpret_cast<const float4*>(bias + co0 + n * 16);
+        f32x4 y[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            float m[4][4];
+#pragma unroll
+            for (int x = 0; x < 16; x++) m[x >> 2][x & 3] = acc[x][n][r];
+            float s0[4], s1[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                s0[j] = m[0][j] + m[1][j] + m[2][j];
+                s1[j] = m[1][j] - m[2][j] - m[3][j];
+            }
+            const float br = r == 0 ? bb.x : r == 1 ? bb.y : r == 2 ? bb.z : bb.w;
+            y[0][r] = (s0[0] + s0[1] + s0[2]) + br;
+            y[1][r] = (s0[1] - s0[2] - s0[3]) + br;
+            y[2][r] = (s1[0] + s1[1] + s1[2]) + br;
+            y[3][r] = (s1[1] - s1[2] - s1[3]) + br;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            f32x4 v = y[q];
+            if constexpr (RESID) v += xres[n][q];
+#pragma unroll
+            for (int r = 0; r < 4; r++) v[r] = fmaxf(v[r], 0.0f);
+            *reinterpret_cast<f32x4*>(ldsb + out_addr(n, q >> 1, q & 1)) = v;
+        }
+    }
+    __syncthreads();
+}
+
+template <bool SEARCH>
+__global__ void __launch_bounds__(512)
+tower32w_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __restrict__ count_ptr, int rows,
+                float* __restrict__ pol_out, float* __restrict__ val_out, SearchOut so) {
+    constexpr int F = 256, NT = 512, NCO = 2;
+    constexpr int RSF = F / 4 + 2, RSI = 32 / 4 + 2;
+    constexpr int XSZ = 64 * RSF;                        // ACT, uint4 slots
+    constexpr int VSZ = 2 * WINO_VBYTES / 16;            // both V buffers (also planes staging, heads scratch)
+    constexpr int ZN = 16 + F / 4;
+    static_assert(HeadsScratch<1, NT>::FLOATS * 4 <= VSZ * 16, "heads scratch must fit in V");
+    static_assert(64 * RSI <= VSZ, "input planes must fit in V");
+    __shared__ __attribute__((aligned(16))) uint4 lds[XSZ + VSZ + ZN];
+    const int count = count_ptr ? min(load_fresh(count_ptr), rows) : rows;
+    const int row0 = blockIdx.x;
+    if (row0 >= count) return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    uint4* X = lds;
+    uint4* V = lds + XSZ;
+    const int vbase = XSZ * 16;
+    const int zero_off = (XSZ + VSZ) * 16;
+    char* ldsb = reinterpret_cast<char*>(lds);
+    stage_planes_f32<1, RSI, NT>(V, planes, so, row0, 1, tid);
+    for (int c = tid; c < ZN; c += NT) lds[XSZ + VSZ + c] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    {   // input conv 19 (32) -> 256: direct (18 k-steps)
+        f32x4 wr[T32_PF][NCO];
+        const __amdgpu_buffer_rsrc_t r0 = t32_rsrc(ta.w[0], ta.wbytes[0]);
+        const __amdgpu_buffer_rsrc_t rz = t32_rsrc(ta.w[0] + 18 * (F / 16) * 64, ta.wbytes[0] - 18 * (F / 16) * 1024);
+        const int voff = ((w * NCO) * 64 + lane) * 16;
+#pragma unroll
+        for (int i = 0; i < T32_PF; i++)
+#pragma unroll
+            for (int n = 0; n < NCO; n++)
+                wr[i][n] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                         r0, voff + n * 1024 + i * (F / 16) * 1024, 0, 0));
+        conv32_lds<32, RSI, F, RSF, 1, NCO, false>(ldsb, reinterpret_cast<char*>(X), vbase, zero_off, r0, rz, ta.b[0],
+                                                   wr, w, 0, lane);
+    }
+    f32x4 xres[2][4];
+    for (int b = 0; b < ta.blocks; b++) {
+        conv_wino<false>(ldsb, vbase, zero_off, t32_rsrc(ta.ww[2 * b], ta.wwbytes[2 * b]), ta.b[1 + 2 * b], xres, w,
+                         lane);
+        conv_wino<true>(ldsb, vbase, zero_off, t32_rsrc(ta.ww[2 * b + 1], ta.wwbytes[2 * b + 1]), ta.b[2 + 2 * b],
+                        xres, w, lane);
+    }
+    heads_group<F, RSF, 1, NT, SEARCH, true>(ldsb, reinterpret_cast<float*>(V), 0, 1, row0, tid, ta.head_frag32, ta.head,
+                                             pol_out, val_out, so, nullptr);
+}
+
+
 bool tower_supported(const NetDev* n) {
     return (n->dtype == AZ_DTYPE_BF16 || n->dtype == AZ_DTYPE_F32) && n->blocks <= 40 &&
            (n->filters == 256 || n->filters == 128 || n->filters == 64 || n->filters == 32);
@@ -981,6 +1223,10 @@ int tower_forward(NetDev* n, const void* planes, const int* count, int rows, flo
     ta.head_frag = reinterpret_cast<const uint4*>(n->head_frag);
     ta.head_frag32 = reinterpret_cast<const uint4*>(n->head_frag32);
     for (int i = 0; i < 1 + 2 * n->blocks; i++) ta.wbytes[i] = (unsigned)n->conv_bytes[i];
+    for (size_t i = 0; i < n->wino_w.size(); i++) {
+        ta.ww[i] = reinterpret_cast<const uint4*>(n->wino_w[i]);
+        ta.wwbytes[i] = (unsigned)n->wino_bytes[i];
+    }
     ta.blocks = n->blocks;
 #ifdef AZ_TOWER_TRACE
     // experiment only: stamp launch number AZ_TOWER_TRACE of this process into $AZ_TOWER_TRACE_FILE
@@ -1027,6 +1273,12 @@ int tower_forward(NetDev* n, const void* planes, const int* count, int rows, flo
         return hipGetLastError() == hipSuccess ? 0 : fail("f32 tower launch failed");                          \
     }
     if (n->dtype == AZ_DTYPE_F32) {
+        if (n->filters == 256 && n->winograd && (int)n->wino_w.size() == 2 * n->blocks) {
+            const int grid = rows;
+            if (so) tower32w_kernel<true><<<grid, 512, 0, st>>>((const float*)planes, ta, count, rows, pol, val, s);
+            else tower32w_kernel<false><<<grid, 512, 0, st>>>((const float*)planes, ta, count, rows, pol, val, s);
+            return hipGetLastError() == hipSuccess ? 0 : fail("f32 Winograd tower launch failed");
+        }
         AZ_TOWER32(256) AZ_TOWER32(128) AZ_TOWER32(64) AZ_TOWER32(32)
         return fail("fused tower: unsupported filters");
     }
