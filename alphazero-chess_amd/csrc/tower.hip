@@ -75,12 +75,14 @@ struct TowerArgs {
     const uint4* ww[2 * 40];       // f32 Winograd weights of the residual convs (F = 256, tower32w_kernel)
     unsigned wwbytes[2 * 40];
     int blocks;
-#ifdef AZ_TOWER_TRACE
+#if defined(AZ_TOWER_TRACE) || defined(AZ_WINO_TRACE)
     unsigned long long* trace;     // experiment only: [grid][TR_SLOTS] s_memrealtime stamps (100 MHz)
 #endif
 };
+#if defined(AZ_TOWER_TRACE) || defined(AZ_WINO_TRACE)
+constexpr int TR_SLOTS = 256;
+#endif
 #ifdef AZ_TOWER_TRACE
-constexpr int TR_SLOTS = 128;
 #define TR_STAMP(k)                                                                                  \
     do {                                                                                             \
         if (tid == 0) ta.trace[(size_t)blockIdx.x * TR_SLOTS + (k)] = __builtin_amdgcn_s_memrealtime(); \
@@ -989,7 +991,7 @@ tower32_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __rest
 #define AZ_WINO_PF 2
 #endif
 #ifndef AZ_WINO_LA
-#define AZ_WINO_LA 2
+#define AZ_WINO_LA 4
 #endif
 #ifndef AZ_WINO_TLOAD
 #define AZ_WINO_TLOAD 0    // step of a chunk at which the next chunk's patch reads issue
@@ -1003,86 +1005,107 @@ constexpr int WINO_LA = AZ_WINO_LA;
 constexpr int WINO_CH = 32;                           // input channels per transform chunk
 constexpr int WINO_VBYTES = 16 * (WINO_CH / 4) * 16 * 16;   // 32 KB per V buffer
 
-template <bool RESID>
+// NWV waves per workgroup (8: two per SIMD, 32 output channels each; 4: one per SIMD, 64 output
+// channels each -- no co-resident wave to share the matrix pipe with, so no arbitration skew at
+// the chunk barriers, and the wave may hold 512 registers); NN = 16-channel output fragments per wave
+template <int NWV> struct WinoCfg {
+    static constexpr int NN = 16 / NWV;                          // output fragments per wave
+    static constexpr int IT = WINO_CH * 16 / (NWV * 64);         // transform items per thread per chunk
+};
+#ifndef AZ_WINO_NWV
+#define AZ_WINO_NWV 8
+#endif
+
+// wr: the weight ring; holds this conv's first WINO_PF steps on entry and the next conv's (rN)
+// on exit, so no layer starts on a cold weight fetch
+template <int NWV, bool RESID>
 __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase, int zero_off,
-                                          const __amdgpu_buffer_rsrc_t rW, const float* __restrict__ bias,
-                                          f32x4 (&xres)[2][4], int w, int lane) {
+                                          const __amdgpu_buffer_rsrc_t rW, const __amdgpu_buffer_rsrc_t rN,
+                                          const float* __restrict__ bias, f32x4 (&wr)[WINO_PF][WinoCfg<NWV>::NN],
+                                          f32x4 (&xres)[WinoCfg<NWV>::NN][4], int w, int lane,
+                                          unsigned long long* trw = nullptr) {
+    // trw (experiment, -DAZ_WINO_TRACE): s_memtime stamps of this wave: [0] entry, [1] after the
+    // prologue barrier, [2 + 2c] chunk c's MFMAs issued, [3 + 2c] after its barrier, [18] epilogue done, [19] exit
+#define WT_STAMP(k) do { if (trw && lane == 0) trw[k] = __builtin_amdgcn_s_memtime(); } while (0)
     constexpr int F = 256, CF = F / 16, RS = F / 4 + 2;
+    constexpr int NN = WinoCfg<NWV>::NN, IT = WinoCfg<NWV>::IT;
     constexpr int NCHUNK = F / WINO_CH, SPC = (WINO_CH / 16) * 16;   // 8 chunks x 32 steps
     constexpr int PF = WINO_PF, LA = WINO_LA;
     static_assert(SPC % PF == 0 && SPC % LA == 0, "ring slots must be compile-time");
     const int l16 = lane & 15, h = lane >> 4;
     const int ty = l16 >> 2, tx = l16 & 3;
-    // transform item of this thread: input channel 4w + h of the chunk, tile l16
-    const int tci4 = (4 * w + h) * 4;
-    const int vwr = w * 256 + l16 * 16 + h * 4;          // + xi * 2048
+    // transform items of this thread: chunk channel 4w + h + 4 NWV it, tile l16 (it < IT)
     const int vrd = h * 256 + l16 * 16;                  // + xi * 2048 + k * 1024
-    // V[buf] <- B^T d B of chunk c for this thread's item, in two halves: tload issues the 16
-    // patch reads, tstore (WINO_TSPLIT steps later, their latency hidden behind MFMAs) transforms
-    // and writes
-    auto tload = [&](int c, float (&d)[4][4]) {
+    // V[buf] <- B^T d B of chunk c for this thread's items, in two halves: tload issues the patch
+    // reads, tstore (WINO_TSPLIT steps later, their latency hidden behind MFMAs) transforms and writes
+    auto tload = [&](int c, float (&d)[IT][4][4]) {
         // patch addresses recomputed per chunk from a laundered tile index: hoisted out of the
         // chunk loop they were 16 loop-invariant registers, and spilled
         const int tl = vgpr_index(l16);
         const int pty = 2 * (tl >> 2) - 1, ptx = 2 * (tl & 3) - 1;
-        const int chan = c * WINO_CH * 4 + tci4;
 #pragma unroll
-        for (int i = 0; i < 4; i++)
+        for (int it = 0; it < IT; it++) {
+            const int chan = (c * WINO_CH + 4 * w + h + 4 * NWV * it) * 4;
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int py = pty + i, px = ptx + j;
+                    const bool ok = (unsigned)py < 8u && (unsigned)px < 8u;
+                    d[it][i][j] = *reinterpret_cast<const float*>(ldsb + (ok ? (py * 8 + px) * RS * 16 : zero_off) + chan);
+                }
+        }
+    };
+    auto tstore = [&](int buf, const float (&d)[IT][4][4]) {
+#pragma unroll
+        for (int it = 0; it < IT; it++) {
+            float t[4][4];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                const int py = pty + i, px = ptx + j;
-                const bool ok = (unsigned)py < 8u && (unsigned)px < 8u;
-                d[i][j] = *reinterpret_cast<const float*>(ldsb + (ok ? (py * 8 + px) * RS * 16 : zero_off) + chan);
+                t[0][j] = d[it][0][j] - d[it][2][j];
+                t[1][j] = d[it][1][j] + d[it][2][j];
+                t[2][j] = d[it][2][j] - d[it][1][j];
+                t[3][j] = d[it][1][j] - d[it][3][j];
             }
-    };
-    auto tstore = [&](int buf, const float (&d)[4][4]) {
-        float t[4][4];
+            // channel 4w + h + 4 NWV it of the chunk -> quad w + NWV it, component h
+            char* vb = ldsb + vbase + buf * WINO_VBYTES + (w + NWV * it) * 256 + l16 * 16 + h * 4;
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            t[0][j] = d[0][j] - d[2][j];
-            t[1][j] = d[1][j] + d[2][j];
-            t[2][j] = d[2][j] - d[1][j];
-            t[3][j] = d[1][j] - d[3][j];
-        }
-        char* vb = ldsb + vbase + buf * WINO_VBYTES + vwr;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const float v0 = t[i][0] - t[i][2], v1 = t[i][1] + t[i][2], v2 = t[i][2] - t[i][1], v3 = t[i][1] - t[i][3];
-            *reinterpret_cast<float*>(vb + (i * 4 + 0) * 2048) = v0;
-            *reinterpret_cast<float*>(vb + (i * 4 + 1) * 2048) = v1;
-            *reinterpret_cast<float*>(vb + (i * 4 + 2) * 2048) = v2;
-            *reinterpret_cast<float*>(vb + (i * 4 + 3) * 2048) = v3;
+            for (int r = 0; r < 4; r++) {
+                const float v0 = t[r][0] - t[r][2], v1 = t[r][1] + t[r][2], v2 = t[r][2] - t[r][1], v3 = t[r][1] - t[r][3];
+                *reinterpret_cast<float*>(vb + (r * 4 + 0) * 2048) = v0;
+                *reinterpret_cast<float*>(vb + (r * 4 + 1) * 2048) = v1;
+                *reinterpret_cast<float*>(vb + (r * 4 + 2) * 2048) = v2;
+                *reinterpret_cast<float*>(vb + (r * 4 + 3) * 2048) = v3;
+            }
         }
     };
     // the residual: this wave's outputs of the block input, read before it is overwritten
-    const int co0 = w * 32 + h * 4;
+    const int co0 = w * 16 * NN + h * 4;
     auto out_addr = [&](int n, int a, int b) { return ((2 * ty + a) * 8 + 2 * tx + b) * RS * 16 + (co0 + n * 16) * 4; };
     if constexpr (!RESID) {
 #pragma unroll
-        for (int n = 0; n < 2; n++)
+        for (int n = 0; n < NN; n++)
 #pragma unroll
             for (int q = 0; q < 4; q++) xres[n][q] = *reinterpret_cast<const f32x4*>(ldsb + out_addr(n, q >> 1, q & 1));
     }
-    f32x4 acc[16][2];
+    WT_STAMP(0);
+    f32x4 acc[16][NN];
 #pragma unroll
-    for (int x = 0; x < 16; x++) { acc[x][0] = f32x4{0.f, 0.f, 0.f, 0.f}; acc[x][1] = f32x4{0.f, 0.f, 0.f, 0.f}; }
-    // weight ring: steps t (16-channel group kc, xi) = kc * 16 + xi; wave w's two fragments at co/16 = 2w, 2w+1
-    const int voff = (2 * w * 64 + lane) * 16;
-    f32x4 wr[PF][2];
+    for (int x = 0; x < 16; x++)
 #pragma unroll
-    for (int i = 0; i < PF; i++)
-#pragma unroll
-        for (int n = 0; n < 2; n++)
-            wr[i][n] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rW, voff + n * 1024 + i * CF * 1024, 0, 0));
+        for (int n = 0; n < NN; n++) acc[x][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // weight ring: steps t (16-channel group kc, xi) = kc * 16 + xi; this wave's fragments at co/16 = NN w + n
+    const int voff = (NN * w * 64 + lane) * 16;
     {
-        float d0[4][4];
+        float d0[IT][4][4];
         tload(0, d0);
         tstore(0, d0);
     }
     __syncthreads();
+    WT_STAMP(1);
 #pragma unroll 1
     for (int c = 0; c < NCHUNK; c++) {
-        float dn[4][4];
+        float dn[IT][4][4];
         const int vb = vbase + (c & 1) * WINO_VBYTES + vrd;
         const bool more = c + 1 < NCHUNK;
         f32x4 bq[LA];
@@ -1090,36 +1113,44 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase, in
         for (int i = 0; i < LA; i++) bq[i] = *reinterpret_cast<const f32x4*>(ldsb + vb + ((i >> 4) * 1024) + (i & 15) * 2048);
 #pragma unroll
         for (int st = 0; st < SPC; st++) {
-            const int k = st >> 4, x = st & 15;
             const f32x4 B = bq[st % LA];
             if (st + LA < SPC) {
                 const int s2 = st + LA;
                 bq[st % LA] = *reinterpret_cast<const f32x4*>(ldsb + vb + (s2 >> 4) * 1024 + (s2 & 15) * 2048);
             }
-            f32x4 a[2] = {wr[st % PF][0], wr[st % PF][1]};
-            {
-                const int tn = c * SPC + st + PF;             // past the conv: its zero pad
+            f32x4 a[NN];
 #pragma unroll
-                for (int n = 0; n < 2; n++)
+            for (int n = 0; n < NN; n++) a[n] = wr[st % PF][n];
+            {
+                // past this conv's last step the refills read the next conv's first steps
+                const int tn = c * SPC + st + PF;
+                const bool nxt = st + PF >= SPC && !more;
+                const int to = nxt ? tn - NCHUNK * SPC : tn;
+#pragma unroll
+                for (int n = 0; n < NN; n++)
                     wr[st % PF][n] = __builtin_bit_cast(
-                        f32x4, __builtin_amdgcn_raw_buffer_load_b128(rW, voff + n * 1024 + tn * CF * 1024, 0, 0));
+                        f32x4, __builtin_amdgcn_raw_buffer_load_b128(nxt ? rN : rW, voff + n * 1024 + to * CF * 1024, 0, 0));
             }
             __builtin_amdgcn_sched_barrier(0);
+            const int x = st & 15;
 #pragma unroll
             for (int s4 = 0; s4 < 4; s4++)
 #pragma unroll
-                for (int n = 0; n < 2; n++)
+                for (int n = 0; n < NN; n++)
                     acc[x][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[n][s4], B[s4], acc[x][n], 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
-            (void)k;
+#ifndef AZ_WINO_NOTRANSFORM   // experiment only: no input transforms inside the chunk loop (wrong results)
             if (st == WINO_TLOAD && more) tload(c + 1, dn);
             if (st == WINO_TLOAD + WINO_TSPLIT && more) tstore((c + 1) & 1, dn);
+#endif
         }
+        WT_STAMP(2 + 2 * c);
         __syncthreads();
+        WT_STAMP(3 + 2 * c);
     }
     // output transform Y = A^T M A per (output fragment n, channel r), + bias (+ residual), ReLU
 #pragma unroll
-    for (int n = 0; n < 2; n++) {
+    for (int n = 0; n < NN; n++) {
         const float4 bb = *reinterpret_cast<const float4*>(bias + co0 + n * 16);
         f32x4 y[4];
 #pragma unroll
@@ -1148,14 +1179,17 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase, in
             *reinterpret_cast<f32x4*>(ldsb + out_addr(n, q >> 1, q & 1)) = v;
         }
     }
+    WT_STAMP(18);
     __syncthreads();
+    WT_STAMP(19);
+#undef WT_STAMP
 }
 
 template <bool SEARCH>
-__global__ void __launch_bounds__(512)
+__global__ void __launch_bounds__(AZ_WINO_NWV * 64)
 tower32w_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __restrict__ count_ptr, int rows,
                 float* __restrict__ pol_out, float* __restrict__ val_out, SearchOut so) {
-    constexpr int F = 256, NT = 512, NCO = 2;
+    constexpr int F = 256, NWV = AZ_WINO_NWV, NT = NWV * 64, NN = WinoCfg<NWV>::NN;
     constexpr int RSF = F / 4 + 2, RSI = 32 / 4 + 2;
     constexpr int XSZ = 64 * RSF;                        // ACT, uint4 slots
     constexpr int VSZ = 2 * WINO_VBYTES / 16;            // both V buffers (also planes staging, heads scratch)
@@ -1177,30 +1211,53 @@ tower32w_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __res
     for (int c = tid; c < ZN; c += NT) lds[XSZ + VSZ + c] = make_uint4(0, 0, 0, 0);
     __syncthreads();
     {   // input conv 19 (32) -> 256: direct (18 k-steps)
-        f32x4 wr[T32_PF][NCO];
+        f32x4 wr[T32_PF][NN];
         const __amdgpu_buffer_rsrc_t r0 = t32_rsrc(ta.w[0], ta.wbytes[0]);
         const __amdgpu_buffer_rsrc_t rz = t32_rsrc(ta.w[0] + 18 * (F / 16) * 64, ta.wbytes[0] - 18 * (F / 16) * 1024);
-        const int voff = ((w * NCO) * 64 + lane) * 16;
+        const int voff = ((w * NN) * 64 + lane) * 16;
 #pragma unroll
         for (int i = 0; i < T32_PF; i++)
 #pragma unroll
-            for (int n = 0; n < NCO; n++)
+            for (int n = 0; n < NN; n++)
                 wr[i][n] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                                          r0, voff + n * 1024 + i * (F / 16) * 1024, 0, 0));
-        conv32_lds<32, RSI, F, RSF, 1, NCO, false>(ldsb, reinterpret_cast<char*>(X), vbase, zero_off, r0, rz, ta.b[0],
-                                                   wr, w, 0, lane);
+        conv32_lds<32, RSI, F, RSF, 1, NN, false>(ldsb, reinterpret_cast<char*>(X), vbase, zero_off, r0, rz, ta.b[0],
+                                                  wr, w, 0, lane);
     }
-    f32x4 xres[2][4];
+#ifdef AZ_WINO_YPRIO   // experiment: the younger wave of each SIMD pair (w >= 4) issues first
+    if (w >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
+    f32x4 xres[NN][4];
+    f32x4 wring[WINO_PF][NN];
+    if (ta.blocks > 0) {
+        const __amdgpu_buffer_rsrc_t r = t32_rsrc(ta.ww[0], ta.wwbytes[0]);
+        const int voff = (NN * w * 64 + lane) * 16;
+#pragma unroll
+        for (int i = 0; i < WINO_PF; i++)
+#pragma unroll
+            for (int n = 0; n < NN; n++)
+                wring[i][n] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff + n * 1024 + i * (F / 16) * 1024, 0, 0));
+    }
     for (int b = 0; b < ta.blocks; b++) {
-        conv_wino<false>(ldsb, vbase, zero_off, t32_rsrc(ta.ww[2 * b], ta.wwbytes[2 * b]), ta.b[1 + 2 * b], xres, w,
-                         lane);
-        conv_wino<true>(ldsb, vbase, zero_off, t32_rsrc(ta.ww[2 * b + 1], ta.wwbytes[2 * b + 1]), ta.b[2 + 2 * b],
-                        xres, w, lane);
+#ifdef AZ_WINO_TRACE
+        unsigned long long* trw = b == 10 ? ta.trace + (size_t)blockIdx.x * TR_SLOTS + w * 24 : nullptr;
+#else
+        unsigned long long* trw = nullptr;
+#endif
+#ifdef AZ_WINO_NOWEIGHTS   // experiment only: zero-record descriptors drop every weight load (wrong results)
+        const unsigned wb1 = 0, wb2 = 0, wb3 = 0;
+#else
+        const unsigned wb1 = ta.wwbytes[2 * b], wb2 = ta.wwbytes[2 * b + 1];
+        const unsigned wb3 = b + 1 < ta.blocks ? ta.wwbytes[2 * b + 2] : 0u;   // after the last conv: nothing (reads 0)
+#endif
+        const __amdgpu_buffer_rsrc_t r1 = t32_rsrc(ta.ww[2 * b], wb1), r2 = t32_rsrc(ta.ww[2 * b + 1], wb2);
+        const __amdgpu_buffer_rsrc_t r3 = t32_rsrc(b + 1 < ta.blocks ? ta.ww[2 * b + 2] : ta.ww[2 * b + 1], wb3);
+        conv_wino<NWV, false>(ldsb, vbase, zero_off, r1, r2, ta.b[1 + 2 * b], wring, xres, w, lane, trw);
+        conv_wino<NWV, true>(ldsb, vbase, zero_off, r2, r3, ta.b[2 + 2 * b], wring, xres, w, lane);
     }
     heads_group<F, RSF, 1, NT, SEARCH, true>(ldsb, reinterpret_cast<float*>(V), 0, 1, row0, tid, ta.head_frag32, ta.head,
                                              pol_out, val_out, so, nullptr);
 }
-
 
 bool tower_supported(const NetDev* n) {
     return (n->dtype == AZ_DTYPE_BF16 || n->dtype == AZ_DTYPE_F32) && n->blocks <= 40 &&
@@ -1228,7 +1285,10 @@ int tower_forward(NetDev* n, const void* planes, const int* count, int rows, flo
         ta.wwbytes[i] = (unsigned)n->wino_bytes[i];
     }
     ta.blocks = n->blocks;
-#ifdef AZ_TOWER_TRACE
+#if defined(AZ_TOWER_TRACE) || defined(AZ_WINO_TRACE)
+#ifndef AZ_TOWER_TRACE
+#define AZ_TOWER_TRACE AZ_WINO_TRACE
+#endif
     // experiment only: stamp launch number AZ_TOWER_TRACE of this process into $AZ_TOWER_TRACE_FILE
     static unsigned long long* trbuf = nullptr;
     static int launch_no = 0;
@@ -1239,7 +1299,7 @@ int tower_forward(NetDev* n, const void* planes, const int* count, int rows, flo
     SearchOut dummy;
     memset(&dummy, 0, sizeof(dummy));
     const SearchOut& s = so ? *so : dummy;
-#ifdef AZ_TOWER_TRACE
+#if defined(AZ_TOWER_TRACE) || defined(AZ_WINO_TRACE)
 #define TRACE_DUMP(grid)                                                                                   \
     if (dump) {                                                                                            \
         std::vector<unsigned long long> h((size_t)(grid) * TR_SLOTS);                                      \
@@ -1275,8 +1335,9 @@ int tower_forward(NetDev* n, const void* planes, const int* count, int rows, flo
     if (n->dtype == AZ_DTYPE_F32) {
         if (n->filters == 256 && n->winograd && (int)n->wino_w.size() == 2 * n->blocks) {
             const int grid = rows;
-            if (so) tower32w_kernel<true><<<grid, 512, 0, st>>>((const float*)planes, ta, count, rows, pol, val, s);
-            else tower32w_kernel<false><<<grid, 512, 0, st>>>((const float*)planes, ta, count, rows, pol, val, s);
+            if (so) tower32w_kernel<true><<<grid, AZ_WINO_NWV * 64, 0, st>>>((const float*)planes, ta, count, rows, pol, val, s);
+            else tower32w_kernel<false><<<grid, AZ_WINO_NWV * 64, 0, st>>>((const float*)planes, ta, count, rows, pol, val, s);
+            TRACE_DUMP(grid);
             return hipGetLastError() == hipSuccess ? 0 : fail("f32 Winograd tower launch failed");
         }
         AZ_TOWER32(256) AZ_TOWER32(128) AZ_TOWER32(64) AZ_TOWER32(32)
