@@ -82,6 +82,7 @@ SIGNATURES = [
     ("az_net_num_params", C.c_size_t, [C.c_int, C.c_int]),
     ("az_net_create", C.c_int, [P(AzNetDesc), P(C.c_float), C.c_size_t, C.c_int, P(C.c_void_p)]),
     ("az_net_destroy", C.c_int, [C.c_void_p]),
+    ("az_net_tower_kernel", C.c_int, [C.c_void_p, C.c_char_p, C.c_int]),
     ("az_net_load_mpk", C.c_int, [C.c_char_p, C.c_int, C.c_int, P(C.c_float), C.c_size_t]),
     ("az_net_save_mpk", C.c_int, [C.c_char_p, C.c_int, C.c_int, P(C.c_float), C.c_size_t]),
     ("az_net_forward", C.c_int, [C.c_void_p, P(C.c_float), C.c_int, P(C.c_float), P(C.c_float)]),

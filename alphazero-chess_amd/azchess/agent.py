@@ -93,6 +93,17 @@ class AlphaZero:
         # libaz runs the fused tower kernel (f32 or bf16) unless AZ_FUSED_TOWER=0
         self.fused_tower = os.environ.get("AZ_FUSED_TOWER", "1") != "0"
 
+    @property
+    def tower_kernel(self):
+        """Which kernel evaluates this net (libaz's choice: fused f32 Winograd / f32 direct / bf16)."""
+        buf = C.create_string_buffer(128)
+        L.check(L.lib.az_net_tower_kernel(self._h, buf, 128))
+        return buf.value.decode()
+
+    @property
+    def winograd(self):
+        return "Winograd" in self.tower_kernel
+
     def __del__(self):
         try:
             L.lib.az_net_destroy(self._h)

@@ -1034,49 +1034,52 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase, in
     static_assert(SPC % PF == 0 && SPC % LA == 0, "ring slots must be compile-time");
     const int l16 = lane & 15, h = lane >> 4;
     const int ty = l16 >> 2, tx = l16 & 3;
-    // transform items of this thread: chunk channel 4w + h + 4 NWV it, tile l16 (it < IT)
-    const int vrd = h * 256 + l16 * 16;                  // + xi * 2048 + k * 1024
-    // V[buf] <- B^T d B of chunk c for this thread's items, in two halves: tload issues the patch
+    // V[xi][quad cq][tile slot][4]: tile slot = tile ^ 4 (cq & 3), so that both the B-fragment
+    // reads (16 tiles x one quad per 16 lanes) and the transform's 4-byte writes (4 tiles x 16
+    // channels per wave) hit 64 distinct banks
+    const int vrd = h * 256 + ((l16 ^ (4 * h)) * 16);    // + xi * 2048 + k * 1024 (cq = 4k + h, cq & 3 = h)
+    // transform items: wave w covers tile row ty = w & 3 and 16 channels; with 8 waves one item per
+    // thread: channel 16 (w >> 2) + (lane & 15) of the chunk, tile (w & 3, lane >> 4) -- a patch
+    // read then touches 4 tiles of one row x 16 consecutive channels: conflict-free with the ACT row
+    // stride of 8 banks mod 64
+    static_assert(IT == 1, "the transform mapping assumes 8 waves");
+    const int tch = 16 * (w >> 2) + (lane & 15);
+    const int tty = w & 3, ttx = lane >> 4;
+    const int vwr = (tch >> 2) * 256 + (((4 * tty + ttx) ^ (4 * ((tch >> 2) & 3))) * 16) + (tch & 3) * 4;   // + xi * 2048
+    // V[buf] <- B^T d B of chunk c for this thread's item, in two halves: tload issues the patch
     // reads, tstore (WINO_TSPLIT steps later, their latency hidden behind MFMAs) transforms and writes
     auto tload = [&](int c, float (&d)[IT][4][4]) {
-        // patch addresses recomputed per chunk from a laundered tile index: hoisted out of the
-        // chunk loop they were 16 loop-invariant registers, and spilled
-        const int tl = vgpr_index(l16);
-        const int pty = 2 * (tl >> 2) - 1, ptx = 2 * (tl & 3) - 1;
+        // patch addresses recomputed per chunk from a laundered index: hoisted out of the chunk
+        // loop they were 16 loop-invariant registers, and spilled
+        const int tl = vgpr_index(ttx);
+        const int pty = 2 * tty - 1, ptx = 2 * tl - 1;
+        const int chan = (c * WINO_CH + tch) * 4;
 #pragma unroll
-        for (int it = 0; it < IT; it++) {
-            const int chan = (c * WINO_CH + 4 * w + h + 4 * NWV * it) * 4;
-#pragma unroll
-            for (int i = 0; i < 4; i++)
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const int py = pty + i, px = ptx + j;
-                    const bool ok = (unsigned)py < 8u && (unsigned)px < 8u;
-                    d[it][i][j] = *reinterpret_cast<const float*>(ldsb + (ok ? (py * 8 + px) * RS * 16 : zero_off) + chan);
-                }
-        }
-    };
-    auto tstore = [&](int buf, const float (&d)[IT][4][4]) {
-#pragma unroll
-        for (int it = 0; it < IT; it++) {
-            float t[4][4];
+        for (int i = 0; i < 4; i++)
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                t[0][j] = d[it][0][j] - d[it][2][j];
-                t[1][j] = d[it][1][j] + d[it][2][j];
-                t[2][j] = d[it][2][j] - d[it][1][j];
-                t[3][j] = d[it][1][j] - d[it][3][j];
+                const int py = pty + i, px = ptx + j;
+                const bool ok = (unsigned)py < 8u && (unsigned)px < 8u;
+                d[0][i][j] = *reinterpret_cast<const float*>(ldsb + (ok ? (py * 8 + px) * RS * 16 : zero_off) + chan);
             }
-            // channel 4w + h + 4 NWV it of the chunk -> quad w + NWV it, component h
-            char* vb = ldsb + vbase + buf * WINO_VBYTES + (w + NWV * it) * 256 + l16 * 16 + h * 4;
+    };
+    auto tstore = [&](int buf, const float (&d)[IT][4][4]) {
+        float t[4][4];
 #pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const float v0 = t[r][0] - t[r][2], v1 = t[r][1] + t[r][2], v2 = t[r][2] - t[r][1], v3 = t[r][1] - t[r][3];
-                *reinterpret_cast<float*>(vb + (r * 4 + 0) * 2048) = v0;
-                *reinterpret_cast<float*>(vb + (r * 4 + 1) * 2048) = v1;
-                *reinterpret_cast<float*>(vb + (r * 4 + 2) * 2048) = v2;
-                *reinterpret_cast<float*>(vb + (r * 4 + 3) * 2048) = v3;
-            }
+        for (int j = 0; j < 4; j++) {
+            t[0][j] = d[0][0][j] - d[0][2][j];
+            t[1][j] = d[0][1][j] + d[0][2][j];
+            t[2][j] = d[0][2][j] - d[0][1][j];
+            t[3][j] = d[0][1][j] - d[0][3][j];
+        }
+        char* vb = ldsb + vbase + buf * WINO_VBYTES + vwr;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const float v0 = t[r][0] - t[r][2], v1 = t[r][1] + t[r][2], v2 = t[r][2] - t[r][1], v3 = t[r][1] - t[r][3];
+            *reinterpret_cast<float*>(vb + (r * 4 + 0) * 2048) = v0;
+            *reinterpret_cast<float*>(vb + (r * 4 + 1) * 2048) = v1;
+            *reinterpret_cast<float*>(vb + (r * 4 + 2) * 2048) = v2;
+            *reinterpret_cast<float*>(vb + (r * 4 + 3) * 2048) = v3;
         }
     };
     // the residual: this wave's outputs of the block input, read before it is overwritten

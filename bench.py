@@ -33,7 +33,7 @@ PEAK_F32_TFLOPS = 157.3       # MI355X_MICROARCH.md: f32 MFMA = vector peak
 PEAK_HBM_GBS = 8000.0         # MI355X_MICROARCH.md: 8.0 TB/s spec
 # HBM bytes per tower launch from rocprofv3 PMC passes (tools/pmc_run.sh: FETCH_SIZE x2 per the
 # gfx950 correction + WRITE_SIZE), same kernel and per-launch work (2048 rows, 20x256)
-PMC_SUMMARY = {"f32": os.path.join(ROOT, "profiles", "r02_pmc_tower32_summary.json"),
+PMC_SUMMARY = {"f32": os.path.join(ROOT, "profiles", "r02_pmc_tower32w_summary.json"),
                "bf16": os.path.join(ROOT, "profiles", "r01_pmc_tower_v11_summary.json")}
 # mean plies of complete self-play games of this config (tools/game_length.py: 256 games, 20x256
 # random-init seed 42, 800 sims/move, noise + temperature moves, played to the end)
@@ -353,22 +353,31 @@ def main():
         del sp
         return elapsed, dict(zip(("sims", "evals", "terminal", "moves", "depth", "hits", "finished"), tot)), tm, c[0]
 
-    def roofline(tm, dtype, fused):
+    def roofline(tm, dtype, net):
+        """The fused tower over the timed region.  achieved = ALGORITHMIC FLOPs (the direct 3x3
+        convs' 2*64*(171F + 18BF^2) per row, SURVEY 8a A6 without the heads) / tower time.  With the
+        Winograd tower the kernel executes 2.25x fewer multiplies on the 40 residual convs than that
+        algorithmic count, so `frac` can exceed 1; `executed_tflops` / `executed_frac` are the MFMA
+        FLOPs the kernel really issues over the same time (the kernel-efficiency figure)."""
         peak = PEAK_BF16_TFLOPS if dtype == "bf16" else PEAK_F32_TFLOPS
         conv_tflops = tm["conv_flop"] / (tm["conv_ms"] * 1e-3) / 1e12 if tm["conv_ms"] > 0 else 0.0
         traffic, traffic_src = pmc_traffic(G, args.blocks, args.filters, dtype)
-        kname = "tower_kernel" if dtype == "bf16" else "tower32_kernel"
+        kname = net.tower_kernel if net is not None else "none (rehearsal)"
+        wino = net is not None and net.winograd
+        B, Fh = args.blocks, args.filters
+        direct_row = 2.0 * 64.0 * (171.0 * Fh + 18.0 * B * Fh * Fh)
+        exec_row = 2.0 * 64.0 * 171.0 * Fh + (2.0 * 64.0 * 18.0 * B * Fh * Fh / 2.25 if wino else 2.0 * 64.0 * 18.0 * B * Fh * Fh)
+        exec_tflops = conv_tflops * exec_row / direct_row
         return {"bound": "mfma", "achieved": conv_tflops, "peak": peak, "unit": "TFLOP/s",
                 "frac": conv_tflops / peak, "traffic": traffic,
                 "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
-                "kernel": ("%s<%d> (fused input conv + %d residual convs + heads, %s; algorithmic FLOPs = conv "
-                           "FLOPs only), %d launches timed (HIP events on every 8th simulation step)"
-                           % (kname, args.filters, 2 * args.blocks,
-                              "v_mfma_f32_16x16x32_bf16" if dtype == "bf16" else "v_mfma_f32_16x16x4_f32",
-                              tm["conv_launches"]))
-                          if fused else
-                          "conv3x3_kernel<%d,%d> (residual 3x3 conv), %d launches timed" %
-                          (args.filters, args.filters, tm["conv_launches"]),
+                "kernel": "%s: input conv + %d residual convs + heads in one launch, %s; algorithmic FLOPs = direct-conv "
+                          "FLOPs; %d launches timed (HIP events on every 8th simulation step)"
+                          % (kname, 2 * B, "v_mfma_f32_16x16x32_bf16" if dtype == "bf16" else "v_mfma_f32_16x16x4_f32",
+                             tm["conv_launches"]),
+                "executed_tflops": exec_tflops, "executed_frac": exec_tflops / peak,
+                "executed_note": ("Winograd F(2x2,3x3): the residual convs execute 1/2.25 of the algorithmic multiplies"
+                                  if wino else "direct convolution: executed = algorithmic"),
                 "flop_per_launch": tm["conv_flop"] / max(tm["conv_launches"], 1),
                 "avg_ms_per_launch": tm["conv_ms"] / max(tm["conv_launches"], 1)}
 
@@ -381,7 +390,7 @@ def main():
     # leaf on the network
     net = make_net(args.dtype)
     elapsed, tot, tm, sims_rank = phase(net, 0, args.steps, True)
-    fused = net.fused_tower if net is not None else False
+    roof = roofline(tm, args.dtype, net)
     del net
     sims_all, evals_all, term_all = tot["sims"], tot["evals"], tot["terminal"]
     fin_all, moves_all, depth_all = tot["finished"], tot["moves"], tot["depth"]
@@ -394,7 +403,7 @@ def main():
         e16, t16, tm16, _ = phase(net16, 0, bf16_steps, True)
         bf16_res = {"value": t16["sims"] / e16, "unit": "sims/s", "steps": bf16_steps,
                     "ms_per_step": e16 / bf16_steps * 1e3, "dtype": "bf16",
-                    "roofline": roofline(tm16, "bf16", net16.fused_tower if net16 is not None else False),
+                    "roofline": roofline(tm16, "bf16", net16),
                     "tolerance_vs_f32_oracle": TOLERANCE["bf16"],
                     "note": "bf16 weights/activations, f32 accumulate: narrower than the reference's f32, "
                             "reported beside the headline, not as it"}
@@ -446,7 +455,7 @@ def main():
                    "step": "%d simulation steps of every game (a move = %d steps)" % (K, S // K),
                    "fen_cache": "off (measured: 1 % hit rate over a 20-move C3 window, -14 % at C2; DESIGN.md section 6)",
                    "parallelism": "games sharded %d-way, no collective (gloo barrier/max only)" % world},
-        "roofline": roofline(tm, args.dtype, fused),
+        "roofline": roof,
         "tower": {"achieved_tflops": tower_tflops, "frac": tower_tflops / peak,
                   "ms_per_sim_step": tm["tower_ms"] / max(tm["sim_steps"], 1)},
         "tolerance_vs_f32_oracle": TOLERANCE[args.dtype],

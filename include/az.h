@@ -86,6 +86,8 @@ size_t az_net_num_params(int blocks, int filters);
  * BatchNorm folded into the convs (inference mode, model.valid()). */
 int az_net_create(const az_net_desc* desc, const float* weights, size_t n, int device, az_net** out);
 int az_net_destroy(az_net* net);
+/* name of the kernel(s) that evaluate this net (fused f32 Winograd / f32 direct / bf16 / per-layer) */
+int az_net_tower_kernel(az_net* net, char* out, int cap);
 /* burn NamedMpkFileRecorder<FullPrecisionSettings> model files:
  * load_model (main.rs:109-116) -> flat weights for az_net_create / az_trainer_create, and
  * model.save_file (training.rs:269-270) from flat weights.  out/w hold az_net_num_params floats. */
