@@ -1142,6 +1142,9 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase, in
                 for (int n = 0; n < NN; n++)
                     acc[x][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[n][s4], B[s4], acc[x][n], 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
+#ifdef AZ_WINO_TRACE
+            if (c == 3 && (st & 7) == 7) WT_STAMP(20 + (st >> 3));   // chunk 3, after steps 7, 15, 23, 31
+#endif
 #ifndef AZ_WINO_NOTRANSFORM   // experiment only: no input transforms inside the chunk loop (wrong results)
             if (st == WINO_TLOAD && more) tload(c + 1, dn);
             if (st == WINO_TLOAD + WINO_TSPLIT && more) tstore((c + 1) & 1, dn);
