@@ -274,8 +274,7 @@ int az_net_tower_kernel(az_net* net, char* out, int cap) {
     const std::string F = std::to_string(n->filters);
     if (!(n->fused && tower_supported(n))) k = "conv3x3_kernel (per layer) + heads_kernel";
     else if (n->dtype == AZ_DTYPE_BF16) k = "tower_kernel<" + F + "> (bf16, direct 3x3)";
-    else if (n->filters == 256 && n->winograd && (int)n->wino_w.size() == 2 * n->blocks)
-        k = "tower32w_kernel<256> (f32, Winograd F(2x2,3x3) residual convs)";
+    else if (wino_supported(n)) k = "tower32w_kernel<" + F + "> (f32, Winograd F(2x2,3x3) residual convs)";
     else k = "tower32_kernel<" + F + "> (f32, direct 3x3)";
     snprintf(out, (size_t)cap, "%s", k.c_str());
     return 0;

@@ -132,9 +132,9 @@ struct NetDev {
     std::vector<void*> conv_w;      // swizzled MFMA fragments per conv (1 + 2*blocks)
     std::vector<float*> conv_b;     // folded bias per conv
     std::vector<size_t> conv_bytes; // allocation size of each conv_w (incl. the 8 zero k-steps of prefetch pad)
-    std::vector<void*> wino_w;      // f32 F=256: Winograd-transformed residual conv weights (tower32w_kernel)
+    std::vector<void*> wino_w;      // f32 F >= 64: Winograd-transformed residual conv weights (tower32w_kernel)
     std::vector<size_t> wino_bytes;
-    bool winograd = AZ_WINOGRAD_DEFAULT != 0;   // tower32w_kernel for f32 F=256 nets (env AZ_WINOGRAD=0/1)
+    bool winograd = AZ_WINOGRAD_DEFAULT != 0;   // tower32w_kernel for f32 F >= 64 nets (env AZ_WINOGRAD=0/1)
     float* head = nullptr;          // folded head weights (f32)
     void* head_frag = nullptr;      // 1x1 F->40 head conv as bf16 hi/lo MFMA A-fragments (fused tower)
     void* head_frag32 = nullptr;    // the same conv as f32 A-fragments of v_mfma_f32_16x16x4_f32 (f32 fused tower)
@@ -190,6 +190,7 @@ int synth_eval_rows(const int* count, int rows, const SearchOut& so, hipStream_t
 int net_planes_from_host_layout(NetDev* n, const float* d_in, int rows, void* planes, hipStream_t st);
 // fused tower (tower.hip): input conv + residual tower + heads in one launch (bf16 and f32).
 bool tower_supported(const NetDev* n);
+bool wino_supported(const NetDev* n);   // f32, F >= 64, Winograd weights built: tower32w_kernel
 int tower_forward(NetDev* n, const void* planes, const int* count, int rows, float* pol, float* val,
                   const SearchOut* so, hipStream_t st);
 size_t act_bytes(int dtype);

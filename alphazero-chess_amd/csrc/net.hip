@@ -494,7 +494,7 @@ int net_create(const az_net_desc* d, const float* wts, size_t n, int device, Net
             if (hipMemcpy(dw, s.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) return -1;
         }
         net->conv_bytes.push_back(bytes);
-        if (d->dtype == AZ_DTYPE_F32 && F == 256 && cin == F) {   // Winograd F(2x2,3x3) copy for tower32w_kernel
+        if (d->dtype == AZ_DTYPE_F32 && F >= 64 && cin == F) {   // Winograd F(2x2,3x3) copy for tower32w_kernel
             auto u = winograd_f32(wf, F);
             void* du = nullptr;
             if (hipMalloc(&du, u.size() * 4) != hipSuccess) return -1;

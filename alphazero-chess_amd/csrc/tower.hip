@@ -1004,48 +1004,54 @@ constexpr int WINO_PF = AZ_WINO_PF;
 constexpr int WINO_LA = AZ_WINO_LA;
 constexpr int WINO_CH = 32;                           // input channels per transform chunk
 constexpr int WINO_VBYTES = 16 * (WINO_CH / 4) * 16 * 16;   // 32 KB per V buffer
-
-// NWV waves per workgroup (8: two per SIMD, 32 output channels each; 4: one per SIMD, 64 output
-// channels each -- no co-resident wave to share the matrix pipe with, so no arbitration skew at
-// the chunk barriers, and the wave may hold 512 registers); NN = 16-channel output fragments per wave
-template <int NWV> struct WinoCfg {
-    static constexpr int NN = 16 / NWV;                          // output fragments per wave
-    static constexpr int IT = WINO_CH * 16 / (NWV * 64);         // transform items per thread per chunk
-};
 #ifndef AZ_WINO_NWV
 #define AZ_WINO_NWV 8
 #endif
 
+// Per filter count: NWV waves per workgroup, NN 16-channel output fragments per wave, XS Winograd
+// points per ring step.  F = 256: 8 waves (two per SIMD) x 32 output channels, one point per step
+// (two independent accumulator chains per step); F = 128: 8 waves x 16 channels, F = 64: 4 waves (one
+// per SIMD, 512 registers) x 16 channels, two points per step so that a step still carries two
+// independent chains (the f32 MFMA's dependent latency exceeds its issue interval)
+template <int F> struct WinoCfg;
+template <> struct WinoCfg<256> { static constexpr int NWV = AZ_WINO_NWV, NN = 16 / NWV, XS = 1; };
+template <> struct WinoCfg<128> { static constexpr int NWV = 8, NN = 1, XS = 2; };
+template <> struct WinoCfg<64> { static constexpr int NWV = 4, NN = 1, XS = 2; };
 // wr: the weight ring; holds this conv's first WINO_PF steps on entry and the next conv's (rN)
 // on exit, so no layer starts on a cold weight fetch
-template <int NWV, bool RESID>
+template <int F, bool RESID>
 __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase, int zero_off,
                                           const __amdgpu_buffer_rsrc_t rW, const __amdgpu_buffer_rsrc_t rN,
-                                          const float* __restrict__ bias, f32x4 (&wr)[WINO_PF][WinoCfg<NWV>::NN],
-                                          f32x4 (&xres)[WinoCfg<NWV>::NN][4], int w, int lane,
+                                          const float* __restrict__ bias,
+                                          f32x4 (&wr)[WINO_PF][WinoCfg<F>::XS][WinoCfg<F>::NN],
+                                          f32x4 (&xres)[WinoCfg<F>::NN][4], int w, int lane,
                                           unsigned long long* trw = nullptr) {
     // trw (experiment, -DAZ_WINO_TRACE): s_memtime stamps of this wave: [0] entry, [1] after the
     // prologue barrier, [2 + 2c] chunk c's MFMAs issued, [3 + 2c] after its barrier, [18] epilogue done, [19] exit
 #define WT_STAMP(k) do { if (trw && lane == 0) trw[k] = __builtin_amdgcn_s_memtime(); } while (0)
-    constexpr int F = 256, CF = F / 16, RS = F / 4 + 2;
-    constexpr int NN = WinoCfg<NWV>::NN, IT = WinoCfg<NWV>::IT;
-    constexpr int NCHUNK = F / WINO_CH, SPC = (WINO_CH / 16) * 16;   // 8 chunks x 32 steps
-    constexpr int PF = WINO_PF, LA = WINO_LA;
-    static_assert(SPC % PF == 0 && SPC % LA == 0, "ring slots must be compile-time");
+    constexpr int CF = F / 16, RS = F / 4 + 2;
+    constexpr int NWV = WinoCfg<F>::NWV, NN = WinoCfg<F>::NN, XS = WinoCfg<F>::XS;
+    constexpr int IT = WINO_CH * 16 / (NWV * 64);                  // transform items per thread per chunk
+    // t = (16-channel group, xi) pairs per chunk (32); a ring step covers XS of them
+    constexpr int NCHUNK = F / WINO_CH, SPC = (WINO_CH / 16) * 16, SPX = SPC / XS;
+    constexpr int PF = WINO_PF, LA = WINO_LA * XS;
+    static_assert(NN * 16 * NWV == F && IT * NWV * 64 == WINO_CH * 16 && NWV % 4 == 0, "Winograd config");
+    static_assert(SPX % PF == 0 && SPC % LA == 0, "ring slots must be compile-time");
     const int l16 = lane & 15, h = lane >> 4;
     const int ty = l16 >> 2, tx = l16 & 3;
     // V[xi][quad cq][tile slot][4]: tile slot = tile ^ 4 (cq & 3), so that both the B-fragment
     // reads (16 tiles x one quad per 16 lanes) and the transform's 4-byte writes (4 tiles x 16
     // channels per wave) hit 64 distinct banks
     const int vrd = h * 256 + ((l16 ^ (4 * h)) * 16);    // + xi * 2048 + k * 1024 (cq = 4k + h, cq & 3 = h)
-    // transform items: wave w covers tile row ty = w & 3 and 16 channels; with 8 waves one item per
-    // thread: channel 16 (w >> 2) + (lane & 15) of the chunk, tile (w & 3, lane >> 4) -- a patch
-    // read then touches 4 tiles of one row x 16 consecutive channels: conflict-free with the ACT row
+    // transform items: wave w covers tile row ty = w & 3 and 16 channels per item: channel
+    // 16 (w >> 2 + it NWV / 4) + (lane & 15) of the chunk, tile (w & 3, lane >> 4) -- a patch read
+    // then touches 4 tiles of one row x 16 consecutive channels: conflict-free with the ACT row
     // stride of 8 banks mod 64
-    static_assert(IT == 1, "the transform mapping assumes 8 waves");
-    const int tch = 16 * (w >> 2) + (lane & 15);
     const int tty = w & 3, ttx = lane >> 4;
-    const int vwr = (tch >> 2) * 256 + (((4 * tty + ttx) ^ (4 * ((tch >> 2) & 3))) * 16) + (tch & 3) * 4;   // + xi * 2048
+    auto tchan = [&](int it) { return 16 * ((w >> 2) + it * (NWV / 4)) + (lane & 15); };
+    auto vwr = [&](int tch) {   // + xi * 2048
+        return (tch >> 2) * 256 + (((4 * tty + ttx) ^ (4 * ((tch >> 2) & 3))) * 16) + (tch & 3) * 4;
+    };
     // V[buf] <- B^T d B of chunk c for this thread's item, in two halves: tload issues the patch
     // reads, tstore (WINO_TSPLIT steps later, their latency hidden behind MFMAs) transforms and writes
     auto tload = [&](int c, float (&d)[IT][4][4]) {
@@ -1053,33 +1059,39 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase, in
         // loop they were 16 loop-invariant registers, and spilled
         const int tl = vgpr_index(ttx);
         const int pty = 2 * tty - 1, ptx = 2 * tl - 1;
-        const int chan = (c * WINO_CH + tch) * 4;
 #pragma unroll
-        for (int i = 0; i < 4; i++)
+        for (int it = 0; it < IT; it++) {
+            const int chan = (c * WINO_CH + tchan(it)) * 4;
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int py = pty + i, px = ptx + j;
-                const bool ok = (unsigned)py < 8u && (unsigned)px < 8u;
-                d[0][i][j] = *reinterpret_cast<const float*>(ldsb + (ok ? (py * 8 + px) * RS * 16 : zero_off) + chan);
-            }
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int py = pty + i, px = ptx + j;
+                    const bool ok = (unsigned)py < 8u && (unsigned)px < 8u;
+                    d[it][i][j] = *reinterpret_cast<const float*>(ldsb + (ok ? (py * 8 + px) * RS * 16 : zero_off) + chan);
+                }
+        }
     };
     auto tstore = [&](int buf, const float (&d)[IT][4][4]) {
-        float t[4][4];
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            t[0][j] = d[0][0][j] - d[0][2][j];
-            t[1][j] = d[0][1][j] + d[0][2][j];
-            t[2][j] = d[0][2][j] - d[0][1][j];
-            t[3][j] = d[0][1][j] - d[0][3][j];
-        }
-        char* vb = ldsb + vbase + buf * WINO_VBYTES + vwr;
+        for (int it = 0; it < IT; it++) {
+            float t[4][4];
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const float v0 = t[r][0] - t[r][2], v1 = t[r][1] + t[r][2], v2 = t[r][2] - t[r][1], v3 = t[r][1] - t[r][3];
-            *reinterpret_cast<float*>(vb + (r * 4 + 0) * 2048) = v0;
-            *reinterpret_cast<float*>(vb + (r * 4 + 1) * 2048) = v1;
-            *reinterpret_cast<float*>(vb + (r * 4 + 2) * 2048) = v2;
-            *reinterpret_cast<float*>(vb + (r * 4 + 3) * 2048) = v3;
+            for (int j = 0; j < 4; j++) {
+                t[0][j] = d[it][0][j] - d[it][2][j];
+                t[1][j] = d[it][1][j] + d[it][2][j];
+                t[2][j] = d[it][2][j] - d[it][1][j];
+                t[3][j] = d[it][1][j] - d[it][3][j];
+            }
+            char* vb = ldsb + vbase + buf * WINO_VBYTES + vwr(tchan(it));
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const float v0 = t[r][0] - t[r][2], v1 = t[r][1] + t[r][2], v2 = t[r][2] - t[r][1], v3 = t[r][1] - t[r][3];
+                *reinterpret_cast<float*>(vb + (r * 4 + 0) * 2048) = v0;
+                *reinterpret_cast<float*>(vb + (r * 4 + 1) * 2048) = v1;
+                *reinterpret_cast<float*>(vb + (r * 4 + 2) * 2048) = v2;
+                *reinterpret_cast<float*>(vb + (r * 4 + 3) * 2048) = v3;
+            }
         }
     };
     // the residual: this wave's outputs of the block input, read before it is overwritten
@@ -1115,39 +1127,52 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase, in
 #pragma unroll
         for (int i = 0; i < LA; i++) bq[i] = *reinterpret_cast<const f32x4*>(ldsb + vb + ((i >> 4) * 1024) + (i & 15) * 2048);
 #pragma unroll
-        for (int st = 0; st < SPC; st++) {
-            const f32x4 B = bq[st % LA];
-            if (st + LA < SPC) {
-                const int s2 = st + LA;
-                bq[st % LA] = *reinterpret_cast<const f32x4*>(ldsb + vb + (s2 >> 4) * 1024 + (s2 & 15) * 2048);
-            }
-            f32x4 a[NN];
+        for (int st = 0; st < SPX; st++) {
+            f32x4 B[XS];
 #pragma unroll
-            for (int n = 0; n < NN; n++) a[n] = wr[st % PF][n];
+            for (int xs = 0; xs < XS; xs++) {
+                const int t = st * XS + xs;
+                B[xs] = bq[t % LA];
+                if (t + LA < SPC) {
+                    const int s2 = t + LA;
+                    bq[t % LA] = *reinterpret_cast<const f32x4*>(ldsb + vb + (s2 >> 4) * 1024 + (s2 & 15) * 2048);
+                }
+            }
+            f32x4 a[XS][NN];
+#pragma unroll
+            for (int xs = 0; xs < XS; xs++)
+#pragma unroll
+                for (int n = 0; n < NN; n++) a[xs][n] = wr[st % PF][xs][n];
             {
                 // past this conv's last step the refills read the next conv's first steps
-                const int tn = c * SPC + st + PF;
-                const bool nxt = st + PF >= SPC && !more;
-                const int to = nxt ? tn - NCHUNK * SPC : tn;
+                const int tn = c * SPX + st + PF;
+                const bool nxt = st + PF >= SPX && !more;
+                const int to = (nxt ? tn - NCHUNK * SPX : tn) * XS;
 #pragma unroll
-                for (int n = 0; n < NN; n++)
-                    wr[st % PF][n] = __builtin_bit_cast(
-                        f32x4, __builtin_amdgcn_raw_buffer_load_b128(nxt ? rN : rW, voff + n * 1024 + to * CF * 1024, 0, 0));
+                for (int xs = 0; xs < XS; xs++)
+#pragma unroll
+                    for (int n = 0; n < NN; n++)
+                        wr[st % PF][xs][n] = __builtin_bit_cast(
+                            f32x4, __builtin_amdgcn_raw_buffer_load_b128(nxt ? rN : rW,
+                                                                         voff + n * 1024 + (to + xs) * CF * 1024, 0, 0));
             }
             __builtin_amdgcn_sched_barrier(0);
-            const int x = st & 15;
 #pragma unroll
             for (int s4 = 0; s4 < 4; s4++)
 #pragma unroll
-                for (int n = 0; n < NN; n++)
-                    acc[x][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[n][s4], B[s4], acc[x][n], 0, 0, 0);
+                for (int xs = 0; xs < XS; xs++)
+#pragma unroll
+                    for (int n = 0; n < NN; n++) {
+                        const int x = (st * XS + xs) & 15;
+                        acc[x][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[xs][n][s4], B[xs][s4], acc[x][n], 0, 0, 0);
+                    }
             __builtin_amdgcn_sched_barrier(0);
 #ifdef AZ_WINO_TRACE
             if (c == 3 && (st & 7) == 7) WT_STAMP(20 + (st >> 3));   // chunk 3, after steps 7, 15, 23, 31
 #endif
 #ifndef AZ_WINO_NOTRANSFORM   // experiment only: no input transforms inside the chunk loop (wrong results)
-            if (st == WINO_TLOAD && more) tload(c + 1, dn);
-            if (st == WINO_TLOAD + WINO_TSPLIT && more) tstore((c + 1) & 1, dn);
+            if (st == WINO_TLOAD / XS && more) tload(c + 1, dn);
+            if (st == (WINO_TLOAD + WINO_TSPLIT) / XS && more) tstore((c + 1) & 1, dn);
 #endif
         }
         WT_STAMP(2 + 2 * c);
@@ -1191,11 +1216,11 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase, in
 #undef WT_STAMP
 }
 
-template <bool SEARCH>
-__global__ void __launch_bounds__(AZ_WINO_NWV * 64)
+template <int F, bool SEARCH>
+__global__ void __launch_bounds__(WinoCfg<F>::NWV * 64)
 tower32w_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __restrict__ count_ptr, int rows,
                 float* __restrict__ pol_out, float* __restrict__ val_out, SearchOut so) {
-    constexpr int F = 256, NWV = AZ_WINO_NWV, NT = NWV * 64, NN = WinoCfg<NWV>::NN;
+    constexpr int NWV = WinoCfg<F>::NWV, NT = NWV * 64, NN = WinoCfg<F>::NN, XS = WinoCfg<F>::XS;
     constexpr int RSF = F / 4 + 2, RSI = 32 / 4 + 2;
     constexpr int XSZ = 64 * RSF;                        // ACT, uint4 slots
     constexpr int VSZ = 2 * WINO_VBYTES / 16;            // both V buffers (also planes staging, heads scratch)
@@ -1216,7 +1241,7 @@ tower32w_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __res
     stage_planes_f32<1, RSI, NT>(V, planes, so, row0, 1, tid);
     for (int c = tid; c < ZN; c += NT) lds[XSZ + VSZ + c] = make_uint4(0, 0, 0, 0);
     __syncthreads();
-    {   // input conv 19 (32) -> 256: direct (18 k-steps)
+    {   // input conv 19 (32) -> F: direct (18 k-steps)
         f32x4 wr[T32_PF][NN];
         const __amdgpu_buffer_rsrc_t r0 = t32_rsrc(ta.w[0], ta.wbytes[0]);
         const __amdgpu_buffer_rsrc_t rz = t32_rsrc(ta.w[0] + 18 * (F / 16) * 64, ta.wbytes[0] - 18 * (F / 16) * 1024);
@@ -1234,15 +1259,18 @@ tower32w_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __res
     if (w >= 4) __builtin_amdgcn_s_setprio(1);
 #endif
     f32x4 xres[NN][4];
-    f32x4 wring[WINO_PF][NN];
+    f32x4 wring[WINO_PF][XS][NN];
     if (ta.blocks > 0) {
         const __amdgpu_buffer_rsrc_t r = t32_rsrc(ta.ww[0], ta.wwbytes[0]);
         const int voff = (NN * w * 64 + lane) * 16;
 #pragma unroll
         for (int i = 0; i < WINO_PF; i++)
 #pragma unroll
-            for (int n = 0; n < NN; n++)
-                wring[i][n] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff + n * 1024 + i * (F / 16) * 1024, 0, 0));
+            for (int xs = 0; xs < XS; xs++)
+#pragma unroll
+                for (int n = 0; n < NN; n++)
+                    wring[i][xs][n] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                    r, voff + n * 1024 + (i * XS + xs) * (F / 16) * 1024, 0, 0));
     }
     for (int b = 0; b < ta.blocks; b++) {
 #ifdef AZ_WINO_TRACE
@@ -1258,8 +1286,8 @@ tower32w_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __res
 #endif
         const __amdgpu_buffer_rsrc_t r1 = t32_rsrc(ta.ww[2 * b], wb1), r2 = t32_rsrc(ta.ww[2 * b + 1], wb2);
         const __amdgpu_buffer_rsrc_t r3 = t32_rsrc(b + 1 < ta.blocks ? ta.ww[2 * b + 2] : ta.ww[2 * b + 1], wb3);
-        conv_wino<NWV, false>(ldsb, vbase, zero_off, r1, r2, ta.b[1 + 2 * b], wring, xres, w, lane, trw);
-        conv_wino<NWV, true>(ldsb, vbase, zero_off, r2, r3, ta.b[2 + 2 * b], wring, xres, w, lane);
+        conv_wino<F, false>(ldsb, vbase, zero_off, r1, r2, ta.b[1 + 2 * b], wring, xres, w, lane, trw);
+        conv_wino<F, true>(ldsb, vbase, zero_off, r2, r3, ta.b[2 + 2 * b], wring, xres, w, lane);
     }
     heads_group<F, RSF, 1, NT, SEARCH, true>(ldsb, reinterpret_cast<float*>(V), 0, 1, row0, tid, ta.head_frag32, ta.head,
                                              pol_out, val_out, so, nullptr);
@@ -1268,6 +1296,10 @@ tower32w_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __res
 bool tower_supported(const NetDev* n) {
     return (n->dtype == AZ_DTYPE_BF16 || n->dtype == AZ_DTYPE_F32) && n->blocks <= 40 &&
            (n->filters == 256 || n->filters == 128 || n->filters == 64 || n->filters == 32);
+}
+
+bool wino_supported(const NetDev* n) {
+    return n->dtype == AZ_DTYPE_F32 && n->winograd && n->filters >= 64 && (int)n->wino_w.size() == 2 * n->blocks;
 }
 
 int tower_forward(NetDev* n, const void* planes, const int* count, int rows, float* pol, float* val,
@@ -1339,13 +1371,18 @@ int tower_forward(NetDev* n, const void* planes, const int* count, int rows, flo
         return hipGetLastError() == hipSuccess ? 0 : fail("f32 tower launch failed");                          \
     }
     if (n->dtype == AZ_DTYPE_F32) {
-        if (n->filters == 256 && n->winograd && (int)n->wino_w.size() == 2 * n->blocks) {
-            const int grid = rows;
-            if (so) tower32w_kernel<true><<<grid, AZ_WINO_NWV * 64, 0, st>>>((const float*)planes, ta, count, rows, pol, val, s);
-            else tower32w_kernel<false><<<grid, AZ_WINO_NWV * 64, 0, st>>>((const float*)planes, ta, count, rows, pol, val, s);
-            TRACE_DUMP(grid);
-            return hipGetLastError() == hipSuccess ? 0 : fail("f32 Winograd tower launch failed");
+#define AZ_TOWER32W(FF)                                                                                       \
+        if (n->filters == FF) {                                                                                \
+            constexpr int NT = WinoCfg<FF>::NWV * 64;                                                          \
+            if (so) tower32w_kernel<FF, true><<<rows, NT, 0, st>>>((const float*)planes, ta, count, rows, pol, val, s); \
+            else tower32w_kernel<FF, false><<<rows, NT, 0, st>>>((const float*)planes, ta, count, rows, pol, val, s);  \
+            TRACE_DUMP(rows);                                                                                  \
+            return hipGetLastError() == hipSuccess ? 0 : fail("f32 Winograd tower launch failed");             \
         }
+        if (wino_supported(n)) {
+            AZ_TOWER32W(256) AZ_TOWER32W(128) AZ_TOWER32W(64)
+        }
+#undef AZ_TOWER32W
         AZ_TOWER32(256) AZ_TOWER32(128) AZ_TOWER32(64) AZ_TOWER32(32)
         return fail("fused tower: unsupported filters");
     }

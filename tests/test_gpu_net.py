@@ -115,3 +115,21 @@ def test_mpk_model_file_drives_the_engine(require_gpu, tmp_path):
     x = np.stack([A.to_tensor(A.Position.startpos())[0]] * 3)
     a, b = net.forward(x), back.forward(x)
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+@pytest.mark.parametrize("blocks,filters", [(6, 64), (2, 128), (20, 256)])
+def test_winograd_tower_matches_direct_tower(require_gpu, blocks, filters, monkeypatch):
+    """tower32w_kernel<F> (residual convs as Winograd F(2x2,3x3)) against tower32_kernel<F> (direct
+    3x3) on the same f32 weights: f32 rounding only (tolerance as the f32 oracle checks)."""
+    w = A.random_weights(blocks, filters, seed=3)
+    planes = random_planes(41, 13)
+    monkeypatch.setenv("AZ_WINOGRAD", "1")
+    wn = A.AlphaZero(blocks, filters, weights=w, dtype="f32")
+    assert wn.tower_kernel.startswith("tower32w_kernel<%d>" % filters)
+    pw, vw = wn.forward(planes)
+    monkeypatch.setenv("AZ_WINOGRAD", "0")
+    dn = A.AlphaZero(blocks, filters, weights=w, dtype="f32")
+    assert dn.tower_kernel.startswith("tower32_kernel<%d>" % filters)
+    pd, vd = dn.forward(planes)
+    np.testing.assert_allclose(vw, vd, atol=1e-5)
+    np.testing.assert_allclose(pw, pd, rtol=1e-4, atol=1e-8)
