@@ -148,7 +148,7 @@ struct NetDev {
 
 // offsets inside NetDev::head
 struct HeadLayout {
-    size_t w40, b40, p2w, p2b, l1w, l1b, l2w, l2b, total;
+    size_t w40, b40, p2w, p2b, l1w, l1b, l2w, l2b, p2f, total;
     __host__ __device__ static HeadLayout make(int F) {
         HeadLayout L;
         L.w40 = 0;                      // [40][F]: policy_conv_1 (32) then value_conv (8), BN folded
@@ -159,7 +159,8 @@ struct HeadLayout {
         L.l1b = L.l1w + 512 * 64;
         L.l2w = L.l1b + 64;             // [64]
         L.l2b = L.l2w + 64;
-        L.total = L.l2b + 4;
+        L.p2f = L.l2b + 4;              // p2w as MFMA A-fragments [cf 4][lane 64][8] (one 32-byte read per lane)
+        L.total = L.p2f + 4 * 64 * 8;
         return L;
     }
 };

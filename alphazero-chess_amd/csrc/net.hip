@@ -538,6 +538,11 @@ int net_create(const az_net_desc* d, const float* wts, size_t n, int device, Net
     memcpy(&hw[L.l1b], l1b, 64 * 4);
     memcpy(&hw[L.l2w], l2w, 64 * 4);
     hw[L.l2b] = l2b[0];
+    // policy 1x1 32->64 A-fragments: lane (l16, h) of tile cf holds rows cf*16 + l16, channels h + 4 ks
+    for (int cf = 0; cf < 4; cf++)
+        for (int lane = 0; lane < 64; lane++)
+            for (int ks = 0; ks < 8; ks++)
+                hw[L.p2f + ((size_t)cf * 64 + lane) * 8 + ks] = p2w[(cf * 16 + (lane & 15)) * 32 + (lane >> 4) + ks * 4];
     net->head_floats = L.total;
     AZ_HIP(hipMalloc(&net->head, L.total * 4));
     AZ_HIP(hipMemcpy(net->head, hw.data(), L.total * 4, hipMemcpyHostToDevice));

@@ -397,9 +397,11 @@ __device__ __forceinline__ void conv_lds(const char* __restrict__ ldsb, uint4* _
 //   new node's legal edges (agent.rs:112-144, tree.rs:84-104).
 template <int F> struct HeadsCfg { static constexpr int NB = F >= 128 ? 2 : 1; };
 constexpr int HEADS_P1S = 80;                           // p1v1 row stride in floats (conflict-free B reads)
-template <int NB, int NT> struct HeadsScratch {
+// NPART partial value-FC sums per (board, wave): 4 for the 4-wave f32 heads (WIDE)
+constexpr int heads_npart(int NT, bool F32X) { return F32X && NT <= 256 ? 4 : 1; }
+template <int NB, int NT, int NPART = 1> struct HeadsScratch {
     static constexpr int PV = 40 * HEADS_P1S, NW = NT / 64;
-    static constexpr int P1 = 0, LG = P1 + NB * PV, RED = LG + NB * 4096, STAT = RED + NB * NW * 64;
+    static constexpr int P1 = 0, LG = P1 + NB * PV, RED = LG + NB * 4096, STAT = RED + NB * NW * 64 * NPART;
     static constexpr int FLOATS = STAT + NB * (2 * NW + 4);
 };
 
@@ -408,7 +410,8 @@ __device__ __forceinline__ void heads_group(const char* __restrict__ xb, float* 
                                             int row0, int tid, const uint4* __restrict__ hfrag,
                                             const float* __restrict__ head, float* pol_out, float* val_out,
                                             const SearchOut& so, unsigned long long* trh = nullptr) {
-    typedef HeadsScratch<NB, NT> S;
+    constexpr int NPART = heads_npart(NT, F32X);
+    typedef HeadsScratch<NB, NT, NPART> S;
     constexpr int NW = S::NW, PV = S::PV, P1S = HEADS_P1S;
     const HeadLayout L = HeadLayout::make(F);
     const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), h = lane >> 4, l16 = lane & 15;
@@ -416,19 +419,57 @@ __device__ __forceinline__ void heads_group(const char* __restrict__ xb, float* 
     float* lg = scr + S::LG;
     float* red = scr + S::RED;
     float* stat = scr + S::STAT;                        // per board: [NW] max, [NW] sum, value, slot, prior off
+#define HT_STAMP(k) do { if (F32X && trh && tid == 0) trh[k] = __builtin_amdgcn_s_memtime(); } while (0)   // f32 towers only
+    HT_STAMP(3);
     // weights of B and C are fetched into registers first: their latency hides behind A
     constexpr int TPW = 16 * NB / NW;                   // policy tiles per wave
-    constexpr int KP = 512 / NW, KPRE = KP < AZ_HEADS_KPRE ? KP : AZ_HEADS_KPRE;
+    // value-FC rows prefetched per wave: all of them for the f32 towers' 4-wave workgroups (one wave
+    // per SIMD, registers to spare)
+    constexpr int KPMAX = (F32X && NW <= 4) ? 128 : AZ_HEADS_KPRE;
+    constexpr int KP = 512 / NW, KPRE = KP < KPMAX ? KP : KPMAX;
+    // 4-wave f32 heads: the value FC with each lane on 4 output units x every 4th row of the wave's
+    // rows (16-byte coalesced weight reads, 4x fewer load instructions); partial sums per lane group
+    constexpr bool WIDE = F32X && NW <= 4;
+    // f32 with 4 waves: A's first KA 16-channel weight groups are requested before everything else,
+    // so that the 1x1 conv does not wait behind the B / C prefetch
+    constexpr int KA = (F32X && NW <= 4) ? (F / 16 < 4 ? F / 16 : 4) : 0;
+    f32x4 hA[KA > 0 ? KA : 1][3];
+    if constexpr (KA > 0) {
+        if (w < 4 * NB) {
+#pragma unroll
+            for (int kc = 0; kc < KA; kc++)
+#pragma unroll
+                for (int cf = 0; cf < 3; cf++) hA[kc][cf] = __builtin_bit_cast(f32x4, hfrag[(kc * 3 + cf) * 64 + lane]);
+        }
+    }
     float pa[TPW > 0 ? TPW : 1][8];
 #pragma unroll
     for (int k = 0; k < TPW; k++) {
         const int t = w + k * NW, cf = (t >> 2) & 3;
+        if constexpr (KA > 0) {   // 4-wave f32 heads: the fragment copy, one 32-byte read per lane
+            const f32x4* src = reinterpret_cast<const f32x4*>(head + L.p2f + ((size_t)cf * 64 + lane) * 8);
+            const f32x4 lo = src[0], hi = src[1];
 #pragma unroll
-        for (int ks = 0; ks < 8; ks++) pa[k][ks] = head[L.p2w + (cf * 16 + l16) * 32 + h + ks * 4];
+            for (int ks = 0; ks < 4; ks++) {
+                pa[k][ks] = lo[ks];
+                pa[k][ks + 4] = hi[ks];
+            }
+        } else {   // (the wider read costs the 8-wave F = 256 kernel a spill)
+#pragma unroll
+            for (int ks = 0; ks < 8; ks++) pa[k][ks] = head[L.p2w + (cf * 16 + l16) * 32 + h + ks * 4];
+        }
     }
-    float wv[KPRE > 0 ? KPRE : 1];
+    float wv[KPRE > 0 && !WIDE ? KPRE : 1];
+    f32x4 wq[WIDE ? KP / 4 : 1];
+    if constexpr (WIDE) {
 #pragma unroll
-    for (int i = 0; i < KPRE; i++) wv[i] = head[L.l1w + (size_t)(w * KP + i) * 64 + lane];
+        for (int i = 0; i < KP / 4; i++)
+            wq[i] = *reinterpret_cast<const f32x4*>(head + L.l1w + (size_t)(w * KP + 4 * i + h) * 64 + 4 * l16);
+    } else {
+#pragma unroll
+        for (int i = 0; i < KPRE; i++) wv[i] = head[L.l1w + (size_t)(w * KP + i) * 64 + lane];
+    }
+    HT_STAMP(4);
     // A
     for (int sfr = w; sfr < 4 * NB; sfr += NW) {
         const int bb = sfr >> 2, sq = (sfr & 3) * 16 + l16;
@@ -439,8 +480,17 @@ __device__ __forceinline__ void heads_group(const char* __restrict__ xb, float* 
         if constexpr (F32X) {
             // f32 activations: exact f32 products on v_mfma_f32_16x16x4_f32, one 16-channel k-chunk
             // (a float4 per lane) per 4 MFMAs
+#pragma unroll
+            for (int kc = 0; kc < KA; kc++) {
+                const f32x4 Bv = *reinterpret_cast<const f32x4*>(xr + kc * 64);
+#pragma unroll
+                for (int s4 = 0; s4 < 4; s4++)
+#pragma unroll
+                    for (int cf = 0; cf < 3; cf++)
+                        acc[cf] = __builtin_amdgcn_mfma_f32_16x16x4f32(hA[kc][cf][s4], Bv[s4], acc[cf], 0, 0, 0);
+            }
 #pragma unroll 4
-            for (int kc = 0; kc < F / 16; kc++) {
+            for (int kc = KA; kc < F / 16; kc++) {
                 const f32x4 Bv = *reinterpret_cast<const f32x4*>(xr + kc * 64);
 #pragma unroll
                 for (int cf = 0; cf < 3; cf++) {
@@ -463,6 +513,7 @@ __device__ __forceinline__ void heads_group(const char* __restrict__ xb, float* 
                             0);
             }
         }
+        HT_STAMP(5);
 #pragma unroll
         for (int cf = 0; cf < 3; cf++)
 #pragma unroll
@@ -472,7 +523,7 @@ __device__ __forceinline__ void heads_group(const char* __restrict__ xb, float* 
             }
     }
     __syncthreads();
-    if (trh && tid == 0) trh[0] = __builtin_amdgcn_s_memrealtime();
+    if (trh && tid == 0) trh[0] = F32X ? __builtin_amdgcn_s_memtime() : __builtin_amdgcn_s_memrealtime();
     // B
     float mxb[NB];
 #pragma unroll
@@ -495,8 +546,21 @@ __device__ __forceinline__ void heads_group(const char* __restrict__ xb, float* 
                 if (q == bb) mxb[q] = fmaxf(mxb[q], l);
         }
     }
+    HT_STAMP(16);
     // C: value FC, wave w owns K rows [w*KP, (w+1)*KP), lane = output unit
-    {
+    if constexpr (WIDE) {
+        f32x4 a[NB];
+#pragma unroll
+        for (int bb = 0; bb < NB; bb++) a[bb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int i = 0; i < KP / 4; i++) {
+            const int k = w * KP + 4 * i + h, c = 32 + (k >> 6), sq = k & 63;
+#pragma unroll
+            for (int bb = 0; bb < NB; bb++) a[bb] += p1v1[bb * PV + c * P1S + sq] * wq[i];
+        }
+#pragma unroll
+        for (int bb = 0; bb < NB; bb++) *reinterpret_cast<f32x4*>(red + ((bb * NW + w) * 4 + h) * 64 + 4 * l16) = a[bb];
+    } else {
         float a[NB];
 #pragma unroll
         for (int bb = 0; bb < NB; bb++) a[bb] = 0.0f;
@@ -510,6 +574,7 @@ __device__ __forceinline__ void heads_group(const char* __restrict__ xb, float* 
 #pragma unroll
         for (int bb = 0; bb < NB; bb++) red[(bb * NW + w) * 64 + lane] = a[bb];
     }
+    HT_STAMP(17);
 #pragma unroll
     for (int bb = 0; bb < NB; bb++) {
         const float m = t_wave_max(mxb[bb]);
@@ -530,11 +595,11 @@ __device__ __forceinline__ void heads_group(const char* __restrict__ xb, float* 
     if (w < NB) {                                       // wave bb finishes board bb's value head
         const int bb = w;
         float hs = head[L.l1b + lane];
-        for (int i = 0; i < NW; i++) hs += red[(bb * NW + i) * 64 + lane];
+        for (int i = 0; i < NW * NPART; i++) hs += red[(bb * NW * NPART + i) * 64 + lane];
         float hv = t_wave_sum(fmaxf(hs, 0.0f) * head[L.l2w + lane]);
         if (lane == 0) stat[bb * (2 * NW + 4) + 2 * NW] = tanhf(hv + head[L.l2b]);
     }
-    if (trh && tid == 0) trh[1] = __builtin_amdgcn_s_memrealtime();
+    if (trh && tid == 0) trh[1] = F32X ? __builtin_amdgcn_s_memtime() : __builtin_amdgcn_s_memrealtime();
     if constexpr (SEARCH) {                             // thread 0 reserves eval-log slots
         if (tid == 0 && so.log_cap > 0) {
 #pragma unroll
@@ -553,7 +618,7 @@ __device__ __forceinline__ void heads_group(const char* __restrict__ xb, float* 
         }
     }
     __syncthreads();
-    if (trh && tid == 0) trh[2] = __builtin_amdgcn_s_memrealtime();
+    if (trh && tid == 0) trh[2] = F32X ? __builtin_amdgcn_s_memtime() : __builtin_amdgcn_s_memrealtime();
 #pragma unroll
     for (int bb = 0; bb < NB; bb++) {
         if (b0 + bb >= nb) break;
@@ -595,6 +660,7 @@ __device__ __forceinline__ void heads_group(const char* __restrict__ xb, float* 
     }
     __syncthreads();
 }
+#undef HT_STAMP
 
 template <int F, bool SEARCH>
 __global__ void __launch_bounds__((F / (16 * TowerCfg<F>::NCO)) * TowerCfg<F>::WB * 64)
@@ -706,7 +772,7 @@ tower_kernel(const __bf16* __restrict__ planes, TowerArgs ta, const int* __restr
         const uint4* after = b + 1 < ta.blocks ? ta.w[3 + 2 * b] : nullptr;
         const unsigned after_bytes = b + 1 < ta.blocks ? ta.wbytes[3 + 2 * b] : 0u;
 #ifdef AZ_TOWER_TRACE
-        unsigned long long* trw = b == 10 ? ta.trace + (size_t)blockIdx.x * TR_SLOTS + 48 + w * 8 : nullptr;
+        unsigned long long* trw = b == (ta.blocks > 10 ? 10 : ta.blocks - 1) ? ta.trace + (size_t)blockIdx.x * TR_SLOTS + 48 + w * 8 : nullptr;
 #else
         unsigned long long* trw = nullptr;
 #endif
@@ -912,7 +978,7 @@ tower32_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __rest
     constexpr int XSZ = BPB * 64 * RSF;
     constexpr int ZN = 16 + F / 4;
     constexpr int NBH = HeadsCfg<F>::NB < BPB ? HeadsCfg<F>::NB : BPB;
-    constexpr int HSZ0 = (HeadsScratch<NBH, NT>::FLOATS * 4 + 15) / 16;
+    constexpr int HSZ0 = (HeadsScratch<NBH, NT, heads_npart(NT, true)>::FLOATS * 4 + 15) / 16;
     constexpr int HSZ = ((XSZ > HSZ0 ? XSZ : HSZ0) + 15) / 16 * 16;
     static_assert(BPB * 64 * RSI <= HSZ, "input planes must fit in h");
     __shared__ __attribute__((aligned(16))) uint4 lds[XSZ + HSZ + ZN];
@@ -962,7 +1028,7 @@ tower32_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __rest
         conv32_lds<F, RSF, F, RSF, BPW, NCO, true>(ldsb, reinterpret_cast<char*>(X), XSZ * 16, zero_off, r2, r3,
                                                    ta.b[i2], wr, cw, bw, lane);
     }
-    static_assert(HeadsScratch<NBH, NT>::FLOATS * 4 <= HSZ * 16, "heads scratch must fit in h");
+    static_assert(HeadsScratch<NBH, NT, heads_npart(NT, true)>::FLOATS * 4 <= HSZ * 16, "heads scratch must fit in h");
     static_assert((16 * NBH) % (NT / 64) == 0, "policy tiles must divide over the waves");
     for (int b0 = 0; b0 < BPB && b0 < nb; b0 += NBH)
         heads_group<F, RSF, NBH, NT, SEARCH, true>(ldsb, reinterpret_cast<float*>(H), b0, nb, row0, tid,
@@ -1002,54 +1068,81 @@ tower32_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __rest
 constexpr int WINO_TLOAD = AZ_WINO_TLOAD, WINO_TSPLIT = AZ_WINO_TSPLIT;
 constexpr int WINO_PF = AZ_WINO_PF;
 constexpr int WINO_LA = AZ_WINO_LA;
-constexpr int WINO_CH = 32;                           // input channels per transform chunk
-constexpr int WINO_VBYTES = 16 * (WINO_CH / 4) * 16 * 16;   // 32 KB per V buffer
 #ifndef AZ_WINO_NWV
 #define AZ_WINO_NWV 8
 #endif
 
-// Per filter count: NWV waves per workgroup, NN 16-channel output fragments per wave, XS Winograd
-// points per ring step.  F = 256: 8 waves (two per SIMD) x 32 output channels, one point per step
-// (two independent accumulator chains per step); F = 128: 8 waves x 16 channels, F = 64: 4 waves (one
-// per SIMD, 512 registers) x 16 channels, two points per step so that a step still carries two
-// independent chains (the f32 MFMA's dependent latency exceeds its issue interval)
+// Per filter count: NWV waves per workgroup, NN 16-channel output fragments per wave, XH waves per
+// output fragment (each on 16 / XH of the Winograd points), XS points per ring step, CH input
+// channels per transform chunk (V buffer = CH KB), PF ring steps of weight prefetch.
+//   F = 256: 8 waves (two per SIMD) x 32 output channels x all 16 points, one point per step (two
+//            independent accumulator chains per step);
+//   F = 128: 8 waves x 16 channels x 16 points, two points per step (still two chains: the f32
+//            MFMA's dependent latency exceeds its issue interval);
+//   F = 64:  8 waves = 4 output fragments x 2 point halves (xi < 8, xi >= 8): two waves per SIMD to
+//            share the matrix pipe; A^T M A is linear in M, so each wave transforms its half and the
+//            two halves' partial outputs are summed through LDS (2 KB per wave).
 template <int F> struct WinoCfg;
-template <> struct WinoCfg<256> { static constexpr int NWV = AZ_WINO_NWV, NN = 16 / NWV, XS = 1; };
-template <> struct WinoCfg<128> { static constexpr int NWV = 8, NN = 1, XS = 2; };
-template <> struct WinoCfg<64> { static constexpr int NWV = 4, NN = 1, XS = 2; };
+#ifndef AZ_WINO64_PF
+#define AZ_WINO64_PF 2
+#endif
+#ifndef AZ_WINO64_XH
+#define AZ_WINO64_XH 2
+#endif
+template <> struct WinoCfg<256> {
+    static constexpr int NWV = AZ_WINO_NWV, NN = 16 / NWV, XH = 1, XS = 1, CH = 32, PF = WINO_PF;
+};
+template <> struct WinoCfg<128> { static constexpr int NWV = 8, NN = 1, XH = 1, XS = 2, CH = 32, PF = WINO_PF; };
+template <> struct WinoCfg<64> {
+    static constexpr int XH = AZ_WINO64_XH, NWV = 4 * XH, NN = 1, XS = 2, CH = 32, PF = AZ_WINO64_PF;
+};
+// Winograd weight fragment offsets: wave w's lane base (output fragments NN cw.., its point half) and
+// the byte offset of ring step t (16-channel group kl = t / NXI, point t % NXI of the half) of chunk cg
+template <int F> __device__ __forceinline__ int wino_voff(int w, int lane) {
+    constexpr int NCW = WinoCfg<F>::NWV / WinoCfg<F>::XH, NXI = 16 / WinoCfg<F>::XH, CF = F / 16;
+    return (WinoCfg<F>::NN * (w % NCW) * 64 + lane) * 16 + (w / NCW) * NXI * CF * 1024;
+}
+template <int F> __device__ __forceinline__ int wino_toff(int cg, int t) {
+    constexpr int NXI = 16 / WinoCfg<F>::XH, KPC = WinoCfg<F>::CH / 16, CF = F / 16;
+    return ((cg * KPC + t / NXI) * 16 + t % NXI) * CF * 1024;
+}
+
 // wr: the weight ring; holds this conv's first WINO_PF steps on entry and the next conv's (rN)
 // on exit, so no layer starts on a cold weight fetch
 template <int F, bool RESID>
 __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase, int zero_off,
                                           const __amdgpu_buffer_rsrc_t rW, const __amdgpu_buffer_rsrc_t rN,
                                           const float* __restrict__ bias,
-                                          f32x4 (&wr)[WINO_PF][WinoCfg<F>::XS][WinoCfg<F>::NN],
+                                          f32x4 (&wr)[WinoCfg<F>::PF][WinoCfg<F>::XS][WinoCfg<F>::NN],
                                           f32x4 (&xres)[WinoCfg<F>::NN][4], int w, int lane,
                                           unsigned long long* trw = nullptr) {
     // trw (experiment, -DAZ_WINO_TRACE): s_memtime stamps of this wave: [0] entry, [1] after the
     // prologue barrier, [2 + 2c] chunk c's MFMAs issued, [3 + 2c] after its barrier, [18] epilogue done, [19] exit
 #define WT_STAMP(k) do { if (trw && lane == 0) trw[k] = __builtin_amdgcn_s_memtime(); } while (0)
     constexpr int CF = F / 16, RS = F / 4 + 2;
-    constexpr int NWV = WinoCfg<F>::NWV, NN = WinoCfg<F>::NN, XS = WinoCfg<F>::XS;
-    constexpr int IT = WINO_CH * 16 / (NWV * 64);                  // transform items per thread per chunk
-    // t = (16-channel group, xi) pairs per chunk (32); a ring step covers XS of them
-    constexpr int NCHUNK = F / WINO_CH, SPC = (WINO_CH / 16) * 16, SPX = SPC / XS;
-    constexpr int PF = WINO_PF, LA = WINO_LA * XS;
-    static_assert(NN * 16 * NWV == F && IT * NWV * 64 == WINO_CH * 16 && NWV % 4 == 0, "Winograd config");
-    static_assert(SPX % PF == 0 && SPC % LA == 0, "ring slots must be compile-time");
+    constexpr int NWV = WinoCfg<F>::NWV, NN = WinoCfg<F>::NN, XS = WinoCfg<F>::XS, XH = WinoCfg<F>::XH;
+    constexpr int CH = WinoCfg<F>::CH, VBYTES = CH * 1024, XST = CH * 64;   // V buffer, xi stride
+    constexpr int IT = CH * 16 / (NWV * 64);                       // transform items per thread per chunk
+    constexpr int NXI = 16 / XH, NCW = NWV / XH;                    // points per wave, output-fragment waves
+    // t = (16-channel group kl, point xi0 + t % NXI) pairs of this wave per chunk; a ring step covers XS
+    constexpr int NCHUNK = F / CH, KPC = CH / 16, SPC = KPC * NXI, SPX = SPC / XS;
+    constexpr int PF = WinoCfg<F>::PF, LA = WINO_LA * XS;
+    static_assert(NN * 16 * NCW == F && IT * NWV * 64 == CH * 16 && NWV % 4 == 0 && IT >= 1, "Winograd config");
+    static_assert(SPX % PF == 0 && SPC % LA == 0 && NXI % XS == 0, "ring slots must be compile-time");
+    const int cw = w % NCW, xp = w / NCW, xi0 = xp * NXI;        // output fragments NN cw.., point half xp
     const int l16 = lane & 15, h = lane >> 4;
     const int ty = l16 >> 2, tx = l16 & 3;
     // V[xi][quad cq][tile slot][4]: tile slot = tile ^ 4 (cq & 3), so that both the B-fragment
     // reads (16 tiles x one quad per 16 lanes) and the transform's 4-byte writes (4 tiles x 16
     // channels per wave) hit 64 distinct banks
-    const int vrd = h * 256 + ((l16 ^ (4 * h)) * 16);    // + xi * 2048 + k * 1024 (cq = 4k + h, cq & 3 = h)
+    const int vrd = h * 256 + ((l16 ^ (4 * h)) * 16);    // + xi * XST + k * 1024 (cq = 4k + h, cq & 3 = h)
     // transform items: wave w covers tile row ty = w & 3 and 16 channels per item: channel
     // 16 (w >> 2 + it NWV / 4) + (lane & 15) of the chunk, tile (w & 3, lane >> 4) -- a patch read
     // then touches 4 tiles of one row x 16 consecutive channels: conflict-free with the ACT row
     // stride of 8 banks mod 64
     const int tty = w & 3, ttx = lane >> 4;
     auto tchan = [&](int it) { return 16 * ((w >> 2) + it * (NWV / 4)) + (lane & 15); };
-    auto vwr = [&](int tch) {   // + xi * 2048
+    auto vwr = [&](int tch) {   // + xi * XST
         return (tch >> 2) * 256 + (((4 * tty + ttx) ^ (4 * ((tch >> 2) & 3))) * 16) + (tch & 3) * 4;
     };
     // V[buf] <- B^T d B of chunk c for this thread's item, in two halves: tload issues the patch
@@ -1061,7 +1154,7 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase, in
         const int pty = 2 * tty - 1, ptx = 2 * tl - 1;
 #pragma unroll
         for (int it = 0; it < IT; it++) {
-            const int chan = (c * WINO_CH + tchan(it)) * 4;
+            const int chan = (c * CH + tchan(it)) * 4;
 #pragma unroll
             for (int i = 0; i < 4; i++)
 #pragma unroll
@@ -1083,19 +1176,19 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase, in
                 t[2][j] = d[it][2][j] - d[it][1][j];
                 t[3][j] = d[it][1][j] - d[it][3][j];
             }
-            char* vb = ldsb + vbase + buf * WINO_VBYTES + vwr(tchan(it));
+            char* vb = ldsb + vbase + buf * VBYTES + vwr(tchan(it));
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 const float v0 = t[r][0] - t[r][2], v1 = t[r][1] + t[r][2], v2 = t[r][2] - t[r][1], v3 = t[r][1] - t[r][3];
-                *reinterpret_cast<float*>(vb + (r * 4 + 0) * 2048) = v0;
-                *reinterpret_cast<float*>(vb + (r * 4 + 1) * 2048) = v1;
-                *reinterpret_cast<float*>(vb + (r * 4 + 2) * 2048) = v2;
-                *reinterpret_cast<float*>(vb + (r * 4 + 3) * 2048) = v3;
+                *reinterpret_cast<float*>(vb + (r * 4 + 0) * XST) = v0;
+                *reinterpret_cast<float*>(vb + (r * 4 + 1) * XST) = v1;
+                *reinterpret_cast<float*>(vb + (r * 4 + 2) * XST) = v2;
+                *reinterpret_cast<float*>(vb + (r * 4 + 3) * XST) = v3;
             }
         }
     };
     // the residual: this wave's outputs of the block input, read before it is overwritten
-    const int co0 = w * 16 * NN + h * 4;
+    const int co0 = cw * 16 * NN + h * 4;
     auto out_addr = [&](int n, int a, int b) { return ((2 * ty + a) * 8 + 2 * tx + b) * RS * 16 + (co0 + n * 16) * 4; };
     if constexpr (!RESID) {
 #pragma unroll
@@ -1104,13 +1197,13 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase, in
             for (int q = 0; q < 4; q++) xres[n][q] = *reinterpret_cast<const f32x4*>(ldsb + out_addr(n, q >> 1, q & 1));
     }
     WT_STAMP(0);
-    f32x4 acc[16][NN];
+    f32x4 acc[NXI][NN];
 #pragma unroll
-    for (int x = 0; x < 16; x++)
+    for (int x = 0; x < NXI; x++)
 #pragma unroll
         for (int n = 0; n < NN; n++) acc[x][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // weight ring: steps t (16-channel group kc, xi) = kc * 16 + xi; this wave's fragments at co/16 = NN w + n
-    const int voff = (NN * w * 64 + lane) * 16;
+    // weight ring: fragment (16-channel group kc, point xi, co/16 = NN cw + n) at ((kc 16 + xi) CF + co/16) KB
+    const int voff = wino_voff<F>(w, lane);
     {
         float d0[IT][4][4];
         tload(0, d0);
@@ -1121,11 +1214,13 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase, in
 #pragma unroll 1
     for (int c = 0; c < NCHUNK; c++) {
         float dn[IT][4][4];
-        const int vb = vbase + (c & 1) * WINO_VBYTES + vrd;
+        const int vb = vbase + (c & 1) * VBYTES + vrd + xi0 * XST;   // this wave's points
+        // B fragment of this wave's step t: 16-channel group t / NXI of the chunk, point xi0 + t % NXI
+        auto boff = [](int t) { return (t / NXI) * 1024 + (t % NXI) * XST; };
         const bool more = c + 1 < NCHUNK;
         f32x4 bq[LA];
 #pragma unroll
-        for (int i = 0; i < LA; i++) bq[i] = *reinterpret_cast<const f32x4*>(ldsb + vb + ((i >> 4) * 1024) + (i & 15) * 2048);
+        for (int i = 0; i < LA; i++) bq[i] = *reinterpret_cast<const f32x4*>(ldsb + vb + boff(i));
 #pragma unroll
         for (int st = 0; st < SPX; st++) {
             f32x4 B[XS];
@@ -1135,7 +1230,7 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase, in
                 B[xs] = bq[t % LA];
                 if (t + LA < SPC) {
                     const int s2 = t + LA;
-                    bq[t % LA] = *reinterpret_cast<const f32x4*>(ldsb + vb + (s2 >> 4) * 1024 + (s2 & 15) * 2048);
+                    bq[t % LA] = *reinterpret_cast<const f32x4*>(ldsb + vb + boff(s2));
                 }
             }
             f32x4 a[XS][NN];
@@ -1144,17 +1239,18 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase, in
 #pragma unroll
                 for (int n = 0; n < NN; n++) a[xs][n] = wr[st % PF][xs][n];
             {
-                // past this conv's last step the refills read the next conv's first steps
-                const int tn = c * SPX + st + PF;
-                const bool nxt = st + PF >= SPX && !more;
-                const int to = (nxt ? tn - NCHUNK * SPX : tn) * XS;
+                // ring step st + PF: chunk c (+1 past this chunk's end); past this conv's last
+                // step the refills read the next conv's first steps
+                const int cadd = (st + PF) / SPX, sl = (st + PF) % SPX;
+                const bool nxt = cadd > 0 && !more;
+                const int cg = nxt ? 0 : c + cadd;
 #pragma unroll
                 for (int xs = 0; xs < XS; xs++)
 #pragma unroll
                     for (int n = 0; n < NN; n++)
                         wr[st % PF][xs][n] = __builtin_bit_cast(
-                            f32x4, __builtin_amdgcn_raw_buffer_load_b128(nxt ? rN : rW,
-                                                                         voff + n * 1024 + (to + xs) * CF * 1024, 0, 0));
+                            f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                       nxt ? rN : rW, voff + n * 1024 + wino_toff<F>(cg, sl * XS + xs), 0, 0));
             }
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -1163,7 +1259,7 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase, in
                 for (int xs = 0; xs < XS; xs++)
 #pragma unroll
                     for (int n = 0; n < NN; n++) {
-                        const int x = (st * XS + xs) & 15;
+                        const int x = (st * XS + xs) % NXI;
                         acc[x][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[xs][n][s4], B[xs][s4], acc[x][n], 0, 0, 0);
                     }
             __builtin_amdgcn_sched_barrier(0);
@@ -1180,34 +1276,80 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase, in
         WT_STAMP(3 + 2 * c);
     }
     // output transform Y = A^T M A per (output fragment n, channel r), + bias (+ residual), ReLU
+    if constexpr (XH == 1) {
 #pragma unroll
-    for (int n = 0; n < NN; n++) {
-        const float4 bb = *reinterpret_cast<const float4*>(bias + co0 + n * 16);
+        for (int n = 0; n < NN; n++) {
+            const float4 bb = *reinterpret_cast<const float4*>(bias + co0 + n * 16);
+            f32x4 y[4];
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                float m[4][4];
+#pragma unroll
+                for (int x = 0; x < 16; x++) m[x >> 2][x & 3] = acc[x][n][r];
+                float s0[4], s1[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    s0[j] = m[0][j] + m[1][j] + m[2][j];
+                    s1[j] = m[1][j] - m[2][j] - m[3][j];
+                }
+                const float br = r == 0 ? bb.x : r == 1 ? bb.y : r == 2 ? bb.z : bb.w;
+                y[0][r] = (s0[0] + s0[1] + s0[2]) + br;
+                y[1][r] = (s0[1] - s0[2] - s0[3]) + br;
+                y[2][r] = (s1[0] + s1[1] + s1[2]) + br;
+                y[3][r] = (s1[1] - s1[2] - s1[3]) + br;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                f32x4 v = y[q];
+                if constexpr (RESID) v += xres[n][q];
+#pragma unroll
+                for (int r = 0; r < 4; r++) v[r] = fmaxf(v[r], 0.0f);
+                *reinterpret_cast<f32x4*>(ldsb + out_addr(n, q >> 1, q & 1)) = v;
+            }
+        }
+    } else {
+        // two point halves: this wave holds rows a = 2 xp, 2 xp + 1 of M (xi = 4 a + b); its partial
+        // A^T M A, then the half-output of the partner's two channels goes through V (free after the
+        // last chunk's barrier) and this wave finishes channels 2 xp, 2 xp + 1 of its fragment
+        static_assert(XH == 2 && NN == 1, "point halves: one output fragment per wave");
         f32x4 y[4];
 #pragma unroll
         for (int r = 0; r < 4; r++) {
-            float m[4][4];
-#pragma unroll
-            for (int x = 0; x < 16; x++) m[x >> 2][x & 3] = acc[x][n][r];
             float s0[4], s1[4];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                s0[j] = m[0][j] + m[1][j] + m[2][j];
-                s1[j] = m[1][j] - m[2][j] - m[3][j];
+                const float m0 = acc[j][0][r], m1 = acc[4 + j][0][r];
+                s0[j] = xp ? m0 : m0 + m1;                    // A^T row 0 = [1 1 1 0]
+                s1[j] = xp ? -(m0 + m1) : m1;                 // A^T row 1 = [0 1 -1 -1]
             }
-            const float br = r == 0 ? bb.x : r == 1 ? bb.y : r == 2 ? bb.z : bb.w;
-            y[0][r] = (s0[0] + s0[1] + s0[2]) + br;
-            y[1][r] = (s0[1] - s0[2] - s0[3]) + br;
-            y[2][r] = (s1[0] + s1[1] + s1[2]) + br;
-            y[3][r] = (s1[1] - s1[2] - s1[3]) + br;
+            y[0][r] = s0[0] + s0[1] + s0[2];
+            y[1][r] = s0[1] - s0[2] - s0[3];
+            y[2][r] = s1[0] + s1[1] + s1[2];
+            y[3][r] = s1[1] - s1[2] - s1[3];
         }
+        // send channels 2 (1 - xp) + {0, 1}: [q][2] as two 16-byte writes
+        const int ro = xp ? 0 : 2;
+        char* xb = ldsb + vbase + ((cw * 2 + (1 - xp)) * 64 + lane) * 32;
+        *reinterpret_cast<f32x4*>(xb) = f32x4{y[0][ro], y[0][ro + 1], y[1][ro], y[1][ro + 1]};
+        *reinterpret_cast<f32x4*>(xb + 16) = f32x4{y[2][ro], y[2][ro + 1], y[3][ro], y[3][ro + 1]};
+        __syncthreads();
+        const char* rb = ldsb + vbase + ((cw * 2 + xp) * 64 + lane) * 32;
+        const f32x4 g0 = *reinterpret_cast<const f32x4*>(rb), g1 = *reinterpret_cast<const f32x4*>(rb + 16);
+        const float recv[4][2] = {{g0[0], g0[1]}, {g0[2], g0[3]}, {g1[0], g1[1]}, {g1[2], g1[3]}};
+        const int rk = xp ? 2 : 0;
+        const float2 bb = *reinterpret_cast<const float2*>(bias + co0 + rk);
+        typedef __attribute__((ext_vector_type(2))) float f32x2;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            f32x4 v = y[q];
-            if constexpr (RESID) v += xres[n][q];
+            f32x2 v;
 #pragma unroll
-            for (int r = 0; r < 4; r++) v[r] = fmaxf(v[r], 0.0f);
-            *reinterpret_cast<f32x4*>(ldsb + out_addr(n, q >> 1, q & 1)) = v;
+            for (int i = 0; i < 2; i++) {
+                const float own = xp ? y[q][2 + i] : y[q][i];
+                v[i] = (own + recv[q][i]) + (i ? bb.y : bb.x);
+                if constexpr (RESID) v[i] += xp ? xres[0][q][2 + i] : xres[0][q][i];
+                v[i] = fmaxf(v[i], 0.0f);
+            }
+            *reinterpret_cast<f32x2*>(ldsb + out_addr(0, q >> 1, q & 1) + rk * 4) = v;
         }
     }
     WT_STAMP(18);
@@ -1221,11 +1363,13 @@ __global__ void __launch_bounds__(WinoCfg<F>::NWV * 64)
 tower32w_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __restrict__ count_ptr, int rows,
                 float* __restrict__ pol_out, float* __restrict__ val_out, SearchOut so) {
     constexpr int NWV = WinoCfg<F>::NWV, NT = NWV * 64, NN = WinoCfg<F>::NN, XS = WinoCfg<F>::XS;
+    constexpr int NCW = NWV / WinoCfg<F>::XH;             // waves of the direct input conv
     constexpr int RSF = F / 4 + 2, RSI = 32 / 4 + 2;
     constexpr int XSZ = 64 * RSF;                        // ACT, uint4 slots
-    constexpr int VSZ = 2 * WINO_VBYTES / 16;            // both V buffers (also planes staging, heads scratch)
+    constexpr int VSZ = 2 * WinoCfg<F>::CH * 1024 / 16;  // both V buffers (also planes staging, heads scratch)
+    constexpr int PF = WinoCfg<F>::PF;
     constexpr int ZN = 16 + F / 4;
-    static_assert(HeadsScratch<1, NT>::FLOATS * 4 <= VSZ * 16, "heads scratch must fit in V");
+    static_assert(HeadsScratch<1, NT, heads_npart(NT, true)>::FLOATS * 4 <= VSZ * 16, "heads scratch must fit in V");
     static_assert(64 * RSI <= VSZ, "input planes must fit in V");
     __shared__ __attribute__((aligned(16))) uint4 lds[XSZ + VSZ + ZN];
     const int count = count_ptr ? min(load_fresh(count_ptr), rows) : rows;
@@ -1238,43 +1382,57 @@ tower32w_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __res
     const int vbase = XSZ * 16;
     const int zero_off = (XSZ + VSZ) * 16;
     char* ldsb = reinterpret_cast<char*>(lds);
+#ifdef AZ_WINO_TRACE   // coarse per-wave stamps: slots 192 + 16 w + k (k: 0 start, 1 staged, 2 input conv, 3 + b block b, 15 end)
+    unsigned long long* trc = w < 4 ? ta.trace + (size_t)blockIdx.x * TR_SLOTS + 192 + 16 * w : nullptr;   // waves 0-3
+#define WC_STAMP(k) do { if (trc && lane == 0) trc[k] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define WC_STAMP(k) do { } while (0)
+#endif
+    WC_STAMP(0);
     stage_planes_f32<1, RSI, NT>(V, planes, so, row0, 1, tid);
     for (int c = tid; c < ZN; c += NT) lds[XSZ + VSZ + c] = make_uint4(0, 0, 0, 0);
     __syncthreads();
+    WC_STAMP(1);
     {   // input conv 19 (32) -> F: direct (18 k-steps)
-        f32x4 wr[T32_PF][NN];
-        const __amdgpu_buffer_rsrc_t r0 = t32_rsrc(ta.w[0], ta.wbytes[0]);
-        const __amdgpu_buffer_rsrc_t rz = t32_rsrc(ta.w[0] + 18 * (F / 16) * 64, ta.wbytes[0] - 18 * (F / 16) * 1024);
-        const int voff = ((w * NN) * 64 + lane) * 16;
+        // (with point halves, only the first NCW waves: the others meet its closing barrier)
+        if (w < NCW) {
+            f32x4 wr[T32_PF][NN];
+            const __amdgpu_buffer_rsrc_t r0 = t32_rsrc(ta.w[0], ta.wbytes[0]);
+            const __amdgpu_buffer_rsrc_t rz = t32_rsrc(ta.w[0] + 18 * (F / 16) * 64, ta.wbytes[0] - 18 * (F / 16) * 1024);
+            const int voff = ((w * NN) * 64 + lane) * 16;
 #pragma unroll
-        for (int i = 0; i < T32_PF; i++)
+            for (int i = 0; i < T32_PF; i++)
 #pragma unroll
-            for (int n = 0; n < NN; n++)
-                wr[i][n] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                         r0, voff + n * 1024 + i * (F / 16) * 1024, 0, 0));
-        conv32_lds<32, RSI, F, RSF, 1, NN, false>(ldsb, reinterpret_cast<char*>(X), vbase, zero_off, r0, rz, ta.b[0],
-                                                  wr, w, 0, lane);
+                for (int n = 0; n < NN; n++)
+                    wr[i][n] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                             r0, voff + n * 1024 + i * (F / 16) * 1024, 0, 0));
+            conv32_lds<32, RSI, F, RSF, 1, NN, false>(ldsb, reinterpret_cast<char*>(X), vbase, zero_off, r0, rz, ta.b[0],
+                                                      wr, w, 0, lane);
+        } else {
+            __syncthreads();
+        }
     }
 #ifdef AZ_WINO_YPRIO   // experiment: the younger wave of each SIMD pair (w >= 4) issues first
     if (w >= 4) __builtin_amdgcn_s_setprio(1);
 #endif
+    WC_STAMP(2);
     f32x4 xres[NN][4];
-    f32x4 wring[WINO_PF][XS][NN];
+    f32x4 wring[PF][XS][NN];
     if (ta.blocks > 0) {
         const __amdgpu_buffer_rsrc_t r = t32_rsrc(ta.ww[0], ta.wwbytes[0]);
-        const int voff = (NN * w * 64 + lane) * 16;
+        const int voff = wino_voff<F>(w, lane);
 #pragma unroll
-        for (int i = 0; i < WINO_PF; i++)
+        for (int i = 0; i < PF; i++)
 #pragma unroll
             for (int xs = 0; xs < XS; xs++)
 #pragma unroll
                 for (int n = 0; n < NN; n++)
                     wring[i][xs][n] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                                    r, voff + n * 1024 + (i * XS + xs) * (F / 16) * 1024, 0, 0));
+                                                                    r, voff + n * 1024 + wino_toff<F>(0, i * XS + xs), 0, 0));
     }
     for (int b = 0; b < ta.blocks; b++) {
 #ifdef AZ_WINO_TRACE
-        unsigned long long* trw = b == 10 ? ta.trace + (size_t)blockIdx.x * TR_SLOTS + w * 24 : nullptr;
+        unsigned long long* trw = b == (ta.blocks > 10 ? 10 : ta.blocks - 1) ? ta.trace + (size_t)blockIdx.x * TR_SLOTS + w * 24 : nullptr;
 #else
         unsigned long long* trw = nullptr;
 #endif
@@ -1288,9 +1446,17 @@ tower32w_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __res
         const __amdgpu_buffer_rsrc_t r3 = t32_rsrc(b + 1 < ta.blocks ? ta.ww[2 * b + 2] : ta.ww[2 * b + 1], wb3);
         conv_wino<F, false>(ldsb, vbase, zero_off, r1, r2, ta.b[1 + 2 * b], wring, xres, w, lane, trw);
         conv_wino<F, true>(ldsb, vbase, zero_off, r2, r3, ta.b[2 + 2 * b], wring, xres, w, lane);
+        if (b < 12) WC_STAMP(3 + b);
     }
+#ifdef AZ_WINO_TRACE
+    unsigned long long* trh = trc ? trc - 16 * w + 9 : nullptr;   // wave 0's slots 9-11: heads A, C, log slots
+#else
+    unsigned long long* trh = nullptr;
+#endif
     heads_group<F, RSF, 1, NT, SEARCH, true>(ldsb, reinterpret_cast<float*>(V), 0, 1, row0, tid, ta.head_frag32, ta.head,
-                                             pol_out, val_out, so, nullptr);
+                                             pol_out, val_out, so, trh);
+    WC_STAMP(15);
+#undef WC_STAMP
 }
 
 bool tower_supported(const NetDev* n) {
