@@ -304,6 +304,7 @@ __device__ __forceinline__ int move_index_bf(int from, int to, int turn) {
     return plane * 64 + rank * 8 + file;
 }
 
+constexpr int GEN_WAVES = 4;   // waves per workgroup that may run gen_legal_wave (k_step STEP_WPB <= 4)
 __device__ __forceinline__ int gen_legal_wave(const azc::Pos& p, Edge* __restrict__ out, int lane, bool* in_check,
                                            bool* legal_ep, unsigned long long* tr = nullptr) {
     using namespace azc;
@@ -420,11 +421,12 @@ __device__ __forceinline__ int gen_legal_wave(const azc::Pos& p, Edge* __restric
         total += __popcll(mb) << b;
     }
     if (tr && lane == 0) tr[9] = __builtin_amdgcn_s_memtime();
-    auto put = [&](int pos, int f, int to, int fl) {
-        Edge e;
-        e.P = 0.0f; e.W = 0.0f; e.N = 0; e.idx = (uint16_t)(move_index_bf(f, to, us) | fl); e.child = CHILD_NONE;
-        out[pos] = e;
-    };
+    // moves are staged in LDS as (from, to, flag) at their positions -- the serial per-lane loop
+    // (up to 27 targets for a queen) is then a few instructions an iteration -- and written out as
+    // edges by one lane per move (move index computed once per move, coalesced 16-byte stores)
+    __shared__ uint32_t s_mv[GEN_WAVES][MAX_EDGES];
+    uint32_t* mv = s_mv[(threadIdx.x >> 6) % GEN_WAVES];
+    auto put = [&](int pos, int f, int to, int fl) { mv[pos] = (uint32_t)f | (uint32_t)to << 6 | (uint32_t)fl << 4; };
     if (ep_to) put(__popcll(ep_mask & ((1ull << lane) - 1ull)), lane, p.ep, 0);
     while (t) {                                        // this lane's main group, ascending to-squares
         put(mpos++, from, ctz64(t), flag);
@@ -440,8 +442,15 @@ __device__ __forceinline__ int gen_legal_wave(const azc::Pos& p, Edge* __restric
         if (lane == 0 && ooo) put(total + (oo ? 1 : 0), ksq, home, 0);
         total += (oo ? 1 : 0) + (ooo ? 1 : 0);
     }
-    const int base = total;
-    return base;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // this wave's LDS writes before its reads
+    for (int o = lane; o < total; o += 64) {
+        const uint32_t v = mv[o];
+        Edge e;
+        e.P = 0.0f; e.W = 0.0f; e.N = 0; e.child = CHILD_NONE;
+        e.idx = (uint16_t)(move_index_bf((int)(v & 63u), (int)((v >> 6) & 63u), us) | (int)((v >> 4) & (uint32_t)PROMO_FLAG));
+        out[o] = e;
+    }
+    return total;
 }
 
 __device__ __forceinline__ int expand_leaf_wave(const Engine& E, int g, int lane, int* nid_out, int step = -1) {
@@ -653,6 +662,7 @@ __global__ void __launch_bounds__(256) k_backup(Engine E, int step) {
 #define AZ_STEP_WPB 1      // C2 A/B (profiles/r02_ab_movegen_c2_*.log): 1 wave per workgroup +2.5 % over 4 (no barrier wait on the slowest game)
 #endif
 constexpr int STEP_WPB = AZ_STEP_WPB;   // games (waves) per k_step workgroup
+static_assert(STEP_WPB <= GEN_WAVES, "gen_legal_wave stages moves in LDS for at most GEN_WAVES waves");
 #ifdef AZ_STEP_TRACE   // experiment: per-wave phase stamps of step AZ_STEP_TRACE (tools/step_trace.py)
 #define ST_STAMP(k) do { if (step == AZ_STEP_TRACE && lane == 0 && g < E.G) E.trace[(size_t)g * 16 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
 #else

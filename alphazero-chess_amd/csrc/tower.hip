@@ -1119,7 +1119,7 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase, in
     // trw (experiment, -DAZ_WINO_TRACE): s_memtime stamps of this wave: [0] entry, [1] after the
     // prologue barrier, [2 + 2c] chunk c's MFMAs issued, [3 + 2c] after its barrier, [18] epilogue done, [19] exit
 #define WT_STAMP(k) do { if (trw && lane == 0) trw[k] = __builtin_amdgcn_s_memtime(); } while (0)
-    constexpr int CF = F / 16, RS = F / 4 + 2;
+    constexpr int RS = F / 4 + 2;
     constexpr int NWV = WinoCfg<F>::NWV, NN = WinoCfg<F>::NN, XS = WinoCfg<F>::XS, XH = WinoCfg<F>::XH;
     constexpr int CH = WinoCfg<F>::CH, VBYTES = CH * 1024, XST = CH * 64;   // V buffer, xi stride
     constexpr int IT = CH * 16 / (NWV * 64);                       // transform items per thread per chunk
