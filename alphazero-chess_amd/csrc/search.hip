@@ -101,33 +101,47 @@ __device__ __forceinline__ void select_game(const Engine& E, int g, int lane) {
     unsigned long long bytes = 0;
     for (;;) {
         const Node nd = nodes[node];
-        const float sq = E.sqrt_tab[nd.nsum + 1];
+        // sqrt(Nt) in-line (IEEE correctly rounded, as the host's sqrtf of the table it replaces):
+        // one dependent load less per level
+        const float sq = sqrtf((float)(nd.nsum + 1));
         float best = -INFINITY;
-        int bpos = 0x7fffffff;
+        int bpos = 0x7fffffff, bchild = CHILD_NONE;
         for (int e = lane; e < nd.nedges; e += 64) {
             const Edge ed = edges[nd.edge_begin + e];
             const float Nf = (float)ed.N;
             const float u = cp * ed.P * sq / (1.0f + Nf);
             const float q = ed.N > 0 ? ed.W / Nf : 0.0f;
             const float v = q + u;
-            if (v > best) { best = v; bpos = e; }
+            if (v > best) { best = v; bpos = e; bchild = ed.child; }
         }
         // wave argmax, first maximum in `moves` order: the wave max, then the lowest edge index
-        // among the lanes holding it (lane order = edge order while nedges <= 64)
+        // among the lanes holding it (lane order = edge order while nedges <= 64); the winner's
+        // child id comes from the edge record that lane already holds
+        int child;
         {
             const float wmax = wave_max_f32(best);
             const unsigned long long hit = __ballot(best == wmax);
-            if (nd.nedges <= 64) bpos = __builtin_amdgcn_readlane(bpos, (int)__builtin_ctzll(hit));
-            else bpos = wave_min_i32(best == wmax ? bpos : 0x7fffffff);
+            int wl;
+            if (nd.nedges <= 64) {
+                wl = (int)__builtin_ctzll(hit);
+                bpos = __builtin_amdgcn_readlane(bpos, wl);
+            } else {
+                const int mn = wave_min_i32(best == wmax ? bpos : 0x7fffffff);
+                wl = (int)__builtin_ctzll(__ballot(best == wmax && bpos == mn));
+                bpos = mn;
+            }
+            child = hit ? __builtin_amdgcn_readlane(bchild, wl) : CHILD_NONE;
         }
-        bytes += 16ull * nd.nedges + 16ull + 4ull;
+        bytes += 16ull * nd.nedges + 16ull;
         // no edge beat -inf: every value is NaN (a diverged network).  The reference keeps its
         // initial idx (tree.rs:121-131); the engine takes the first edge instead of reading
         // past the node's edge list.
-        if (bpos >= nd.nedges) bpos = 0;
+        if (bpos >= nd.nedges) {
+            bpos = 0;
+            child = edges[nd.edge_begin].child;
+        }
         const int eabs = nd.edge_begin + bpos;
         if (lane == 0) { pn[len] = node; pe[len] = eabs; }
-        const int child = edges[eabs].child;
         len++;
         if (child >= 0 && len < E.PMAX) { node = child; continue; }
         if (lane == 0) {
@@ -627,13 +641,31 @@ __device__ __forceinline__ void backup_stats(const Engine& E, int step) {
 __device__ __forceinline__ void backup_game(const Engine& E, int g, int lane) {
     Node* nodes = game_nodes(E, g);
     Edge* edges = game_edges(E, g);
-    const int kind = E.leaf_kind[g], len = E.leaf_len[g];
-    const float v = kind == LEAF_EVAL ? E.value[E.leaf_row[g]]
-                  : kind == LEAF_CACHED ? E.cached_value[g] : (kind == LEAF_DRAW ? 0.0f : -1.0f);
     const int* pn = E.path_node + (size_t)g * E.PMAX;
     const int* pe = E.path_edge + (size_t)g * E.PMAX;
-    for (int k = lane; k < len; k += 64) {
-        const float val = ((len - 1 - k) & 1) ? v : -v;      // value = -child value per level
+    // two rounds of dependent loads, not four: (1) the leaf record and the path's first 64 levels
+    // (independent of the path length), (2) the leaf value and the edge / node records those levels
+    // name (read speculatively at clamped indices: entries past the length are stale)
+    const int lk = min(lane, E.PMAX - 1);
+    const int p0e = min(max(pe[lk], 0), E.EMAX - 1), p0n = min(max(pn[lk], 0), E.NMAX - 1);
+    const int kind = E.leaf_kind[g], len = E.leaf_len[g], row = E.leaf_row[g];
+    const float ve = E.value[min(max(row, 0), E.G - 1)], vc = E.cached_value[g];
+    Edge* ed0 = edges + p0e;
+    Node* nd0 = nodes + p0n;
+    const float w0 = ed0->W;
+    const uint16_t n0 = ed0->N;
+    const int s0 = nd0->nsum;
+    // a second (never taken) use keeps the compiler from sinking the reads into the update below
+    if (len == -1) E.trace[lane] = (unsigned long long)__builtin_bit_cast(unsigned, w0) + n0 + s0;
+    const float v = kind == LEAF_EVAL ? ve : kind == LEAF_CACHED ? vc : (kind == LEAF_DRAW ? 0.0f : -1.0f);
+    if (lane < len) {
+        const float val = ((len - 1 - lane) & 1) ? v : -v;   // value = -child value per level
+        ed0->W = w0 + val;
+        ed0->N = (uint16_t)(n0 + 1);
+        nd0->nsum = s0 + 1;
+    }
+    for (int k = lane + 64; k < len; k += 64) {
+        const float val = ((len - 1 - k) & 1) ? v : -v;
         Edge* ed = edges + pe[k];
         ed->W = ed->W + val;
         ed->N = (uint16_t)(ed->N + 1);
