@@ -97,6 +97,7 @@ struct Engine {
     Node* nodes;          // [G][NMAX]
     azc::Pos* npos;       // [G][NMAX]
     Edge* edges;          // [G][EMAX]
+    uint32_t* child_hdr;  // [G][EMAX]: for an edge whose child is a node, (child's edge_begin << 8) | nedges
     int* node_count; int* edge_count; int* max_depth;
     int* leaf_node; int* leaf_edge; int* leaf_len; int* leaf_kind; int* leaf_row;
     int* path_node; int* path_edge;        // [G][PMAX]

@@ -75,6 +75,17 @@ __device__ __forceinline__ int wave_min_i32(int v) {
     v = min(v, dpp_i32<0x143, 0xC>(v, v));
     return __builtin_amdgcn_readlane(v, 63);
 }
+// sum over the wave (all lanes active); result wave-uniform.  Lanes outside a row_bcast's row
+// mask keep `old` = 0, so nothing is counted twice.
+__device__ __forceinline__ int wave_sum_i32(int v) {
+    v += dpp_i32<0xB1>(0, v);
+    v += dpp_i32<0x4E>(0, v);
+    v += dpp_i32<0x141>(0, v);
+    v += dpp_i32<0x140>(0, v);
+    v += dpp_i32<0x142, 0xA>(0, v);
+    v += dpp_i32<0x143, 0xC>(0, v);
+    return __builtin_amdgcn_readlane(v, 63);
+}
 // exclusive prefix sum over the wave of a small count (0..31) by its bits: one ballot and one
 // mbcnt per bit; *total = the wave sum (uniform)
 __device__ __forceinline__ int wave_excl_small(int cnt, int* total) {
@@ -97,32 +108,53 @@ __device__ __forceinline__ void select_game(const Engine& E, int g, int lane) {
     int* pn = E.path_node + (size_t)g * E.PMAX;
     int* pe = E.path_edge + (size_t)g * E.PMAX;
     const float cp = E.c_puct;
+    const uint32_t* chdr = E.child_hdr + (size_t)g * E.EMAX;
     int node = 0, len = 0;
     unsigned long long bytes = 0;
+    // the current node's edge range: the root's from its record; below it, from the child_hdr
+    // entry of the edge that leads there, read together with that edge -- one dependent load
+    // round per level.  Nt - 1 = sum of the node's edge visits (= its nsum: every backup adds one
+    // to both), summed on DPP from the edges already loaded.
+    const Node rt = nodes[0];
+    int ebeg = (int)rt.edge_begin, nedg = rt.nedges;
     for (;;) {
-        const Node nd = nodes[node];
-        // sqrt(Nt) in-line (IEEE correctly rounded, as the host's sqrtf of the table it replaces):
-        // one dependent load less per level
-        const float sq = sqrtf((float)(nd.nsum + 1));
         float best = -INFINITY;
         int bpos = 0x7fffffff, bchild = CHILD_NONE;
-        for (int e = lane; e < nd.nedges; e += 64) {
-            const Edge ed = edges[nd.edge_begin + e];
+        uint32_t bhdr = 0u;
+        if (nedg <= 64) {
+            const int e = min(lane, nedg - 1);             // unconditional (clamped) loads
+            const Edge ed = edges[ebeg + e];
+            const uint32_t hd = chdr[ebeg + e];
+            const int nsum = wave_sum_i32(lane < nedg ? (int)ed.N : 0);
+            // sqrt(Nt) in-line (IEEE correctly rounded, as the host's sqrtf in the oracle)
+            const float sq = sqrtf((float)(nsum + 1));
             const float Nf = (float)ed.N;
             const float u = cp * ed.P * sq / (1.0f + Nf);
             const float q = ed.N > 0 ? ed.W / Nf : 0.0f;
             const float v = q + u;
-            if (v > best) { best = v; bpos = e; bchild = ed.child; }
+            if (lane < nedg && v > best) { best = v; bpos = lane; bchild = ed.child; bhdr = hd; }
+        } else {
+            const float sq = sqrtf((float)(nodes[node].nsum + 1));
+            for (int e = lane; e < nedg; e += 64) {
+                const Edge ed = edges[ebeg + e];
+                const uint32_t hd = chdr[ebeg + e];
+                const float Nf = (float)ed.N;
+                const float u = cp * ed.P * sq / (1.0f + Nf);
+                const float q = ed.N > 0 ? ed.W / Nf : 0.0f;
+                const float v = q + u;
+                if (v > best) { best = v; bpos = e; bchild = ed.child; bhdr = hd; }
+            }
         }
         // wave argmax, first maximum in `moves` order: the wave max, then the lowest edge index
         // among the lanes holding it (lane order = edge order while nedges <= 64); the winner's
-        // child id comes from the edge record that lane already holds
+        // child id and child header come from the records that lane already holds
         int child;
+        uint32_t hdr;
         {
             const float wmax = wave_max_f32(best);
             const unsigned long long hit = __ballot(best == wmax);
             int wl;
-            if (nd.nedges <= 64) {
+            if (nedg <= 64) {
                 wl = (int)__builtin_ctzll(hit);
                 bpos = __builtin_amdgcn_readlane(bpos, wl);
             } else {
@@ -130,20 +162,27 @@ __device__ __forceinline__ void select_game(const Engine& E, int g, int lane) {
                 wl = (int)__builtin_ctzll(__ballot(best == wmax && bpos == mn));
                 bpos = mn;
             }
-            child = hit ? __builtin_amdgcn_readlane(bchild, wl) : CHILD_NONE;
+            child = __builtin_amdgcn_readlane(bchild, wl);
+            hdr = (uint32_t)__builtin_amdgcn_readlane((int)bhdr, wl);
         }
-        bytes += 16ull * nd.nedges + 16ull;
+        bytes += 20ull * nedg;
         // no edge beat -inf: every value is NaN (a diverged network).  The reference keeps its
         // initial idx (tree.rs:121-131); the engine takes the first edge instead of reading
         // past the node's edge list.
-        if (bpos >= nd.nedges) {
+        if (bpos >= nedg) {
             bpos = 0;
-            child = edges[nd.edge_begin].child;
+            child = edges[ebeg].child;
+            hdr = chdr[ebeg];
         }
-        const int eabs = nd.edge_begin + bpos;
+        const int eabs = ebeg + bpos;
         if (lane == 0) { pn[len] = node; pe[len] = eabs; }
         len++;
-        if (child >= 0 && len < E.PMAX) { node = child; continue; }
+        if (child >= 0 && len < E.PMAX) {
+            node = child;
+            ebeg = (int)(hdr >> 8);
+            nedg = (int)(hdr & 255u);
+            continue;
+        }
         if (lane == 0) {
             E.leaf_node[g] = node;
             E.leaf_edge[g] = eabs;
@@ -275,6 +314,7 @@ __device__ __forceinline__ int expand_leaf(const Engine& E, int g, int* nid_out)
     npos[nid] = c;
     E.node_count[g] = nid + 1;
     E.edge_count[g] = ebeg + n;
+    E.child_hdr[(size_t)g * E.EMAX + eabs] = (uint32_t)ebeg << 8 | (uint32_t)n;
     edges[eabs].child = nid;
     if (nn.depth > maxd) E.max_depth[g] = nn.depth;
     if (E.cache_mask >= 0) {                                 // FEN cache lookup (tree.rs:214-219)
@@ -551,6 +591,7 @@ __device__ __forceinline__ int expand_leaf_wave(const Engine& E, int g, int lane
         npos[nid] = c;
         E.node_count[g] = nid + 1;
         E.edge_count[g] = ebeg + n;
+        E.child_hdr[(size_t)g * E.EMAX + eabs] = (uint32_t)ebeg << 8 | (uint32_t)n;
         edges[eabs].child = nid;
         if (nn.depth > maxd) E.max_depth[g] = nn.depth;
     }
@@ -1355,12 +1396,14 @@ int az_search_create(az_net* net, const az_search_cfg* cfg, int device, az_searc
     const int G = cfg->games, S = cfg->sims;
     E.G = G; E.S = S; E.NMAX = S + 2; E.PMAX = S + 2;
     E.EMAX = E.NMAX * 218 + MAX_EDGES;
+    // sims <= 60000 (checked above) keeps EMAX < 2^24: child_hdr packs edge_begin in 24 bits
     E.c_puct = cfg->c_puct; E.dir_alpha = cfg->dir_alpha; E.dir_eps = cfg->dir_eps;
     E.temp_moves = cfg->temp_moves; E.noise = cfg->noise; E.continuous = cfg->continuous; E.seed = cfg->seed;
     int rc = 0;
     rc |= dalloc(s, &E.nodes, (size_t)G * E.NMAX);
     rc |= dalloc(s, &E.npos, (size_t)G * E.NMAX);
     rc |= dalloc(s, &E.edges, (size_t)G * E.EMAX);
+    rc |= dalloc(s, &E.child_hdr, (size_t)G * E.EMAX);
     rc |= dalloc(s, &E.node_count, G); rc |= dalloc(s, &E.edge_count, G); rc |= dalloc(s, &E.max_depth, G);
     rc |= dalloc(s, &E.leaf_node, G); rc |= dalloc(s, &E.leaf_edge, G); rc |= dalloc(s, &E.leaf_len, G);
     rc |= dalloc(s, &E.leaf_kind, G); rc |= dalloc(s, &E.leaf_row, G);
