@@ -1072,6 +1072,7 @@ constexpr int WINO_LA = AZ_WINO_LA;
 #define AZ_WINO_NWV 8
 #endif
 
+
 // Per filter count: NWV waves per workgroup, NN 16-channel output fragments per wave, XH waves per
 // output fragment (each on 16 / XH of the Winograd points), XS points per ring step, CH input
 // channels per transform chunk (V buffer = CH KB), PF ring steps of weight prefetch.
@@ -1119,7 +1120,7 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase, in
     // trw (experiment, -DAZ_WINO_TRACE): s_memtime stamps of this wave: [0] entry, [1] after the
     // prologue barrier, [2 + 2c] chunk c's MFMAs issued, [3 + 2c] after its barrier, [18] epilogue done, [19] exit
 #define WT_STAMP(k) do { if (trw && lane == 0) trw[k] = __builtin_amdgcn_s_memtime(); } while (0)
-    constexpr int RS = F / 4 + 2;
+    constexpr int CF = F / 16, RS = F / 4 + 2;
     constexpr int NWV = WinoCfg<F>::NWV, NN = WinoCfg<F>::NN, XS = WinoCfg<F>::XS, XH = WinoCfg<F>::XH;
     constexpr int CH = WinoCfg<F>::CH, VBYTES = CH * 1024, XST = CH * 64;   // V buffer, xi stride
     constexpr int IT = CH * 16 / (NWV * 64);                       // transform items per thread per chunk
@@ -1243,14 +1244,27 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase, in
                 // step the refills read the next conv's first steps
                 const int cadd = (st + PF) / SPX, sl = (st + PF) % SPX;
                 const bool nxt = cadd > 0 && !more;
-                const int cg = nxt ? 0 : c + cadd;
+                if constexpr (XH == 1) {
+                    // one point set: the steps of a conv are linear in the weights
+                    const int tn = c * SPX + st + PF;
+                    const int to = (nxt ? tn - NCHUNK * SPX : tn) * XS;
 #pragma unroll
-                for (int xs = 0; xs < XS; xs++)
+                    for (int xs = 0; xs < XS; xs++)
 #pragma unroll
-                    for (int n = 0; n < NN; n++)
-                        wr[st % PF][xs][n] = __builtin_bit_cast(
-                            f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                       nxt ? rN : rW, voff + n * 1024 + wino_toff<F>(cg, sl * XS + xs), 0, 0));
+                        for (int n = 0; n < NN; n++)
+                            wr[st % PF][xs][n] = __builtin_bit_cast(
+                                f32x4, __builtin_amdgcn_raw_buffer_load_b128(nxt ? rN : rW,
+                                                                             voff + n * 1024 + (to + xs) * CF * 1024, 0, 0));
+                } else {
+                    const int cg = nxt ? 0 : c + cadd;
+#pragma unroll
+                    for (int xs = 0; xs < XS; xs++)
+#pragma unroll
+                        for (int n = 0; n < NN; n++)
+                            wr[st % PF][xs][n] = __builtin_bit_cast(
+                                f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                           nxt ? rN : rW, voff + n * 1024 + wino_toff<F>(cg, sl * XS + xs), 0, 0));
+                }
             }
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -1363,7 +1377,7 @@ __global__ void __launch_bounds__(WinoCfg<F>::NWV * 64)
 tower32w_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __restrict__ count_ptr, int rows,
                 float* __restrict__ pol_out, float* __restrict__ val_out, SearchOut so) {
     constexpr int NWV = WinoCfg<F>::NWV, NT = NWV * 64, NN = WinoCfg<F>::NN, XS = WinoCfg<F>::XS;
-    constexpr int NCW = NWV / WinoCfg<F>::XH;             // waves of the direct input conv
+    constexpr int XH = WinoCfg<F>::XH, NCW = NWV / XH;    // waves of the direct input conv
     constexpr int RSF = F / 4 + 2, RSI = 32 / 4 + 2;
     constexpr int XSZ = 64 * RSF;                        // ACT, uint4 slots
     constexpr int VSZ = 2 * WinoCfg<F>::CH * 1024 / 16;  // both V buffers (also planes staging, heads scratch)
@@ -1394,8 +1408,7 @@ tower32w_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __res
     __syncthreads();
     WC_STAMP(1);
     {   // input conv 19 (32) -> F: direct (18 k-steps)
-        // (with point halves, only the first NCW waves: the others meet its closing barrier)
-        if (w < NCW) {
+        auto input_conv = [&]() {
             f32x4 wr[T32_PF][NN];
             const __amdgpu_buffer_rsrc_t r0 = t32_rsrc(ta.w[0], ta.wbytes[0]);
             const __amdgpu_buffer_rsrc_t rz = t32_rsrc(ta.w[0] + 18 * (F / 16) * 64, ta.wbytes[0] - 18 * (F / 16) * 1024);
@@ -1408,8 +1421,12 @@ tower32w_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __res
                                                              r0, voff + n * 1024 + i * (F / 16) * 1024, 0, 0));
             conv32_lds<32, RSI, F, RSF, 1, NN, false>(ldsb, reinterpret_cast<char*>(X), vbase, zero_off, r0, rz, ta.b[0],
                                                       wr, w, 0, lane);
-        } else {
-            __syncthreads();
+        };
+        if constexpr (XH == 1) {
+            input_conv();
+        } else {   // point halves: only the first NCW waves; the others meet its closing barrier
+            if (w < NCW) input_conv();
+            else __syncthreads();
         }
     }
 #ifdef AZ_WINO_YPRIO   // experiment: the younger wave of each SIMD pair (w >= 4) issues first
