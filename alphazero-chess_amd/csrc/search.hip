@@ -1099,7 +1099,7 @@ template <typename T> int dalloc(az_search* s, T** p, size_t count) {
 }
 
 constexpr int EV_PER_STEP = 9;
-constexpr int TIMING_EVERY = 8;   // sampled simulation steps in timing mode (az_timing)
+constexpr int TIMING_EVERY = 32;  // sampled simulation steps in timing mode (az_timing)
 
 // sum of a per-game device counter (infrequent readouts; the stream is synchronised by the caller)
 unsigned long long sum_games(az_search* s, const unsigned long long* d) {
@@ -1203,8 +1203,9 @@ int run_sims(az_search* s, int i0 = 0, int i1 = -1) {
         }
     }
     // timing mode brackets every TIMING_EVERY-th simulation step with events (an event record
-    // costs a few us of GPU time: on every step it was ~20 % of a 6x64 simulation step); those
-    // steps run as separate kernels, the others through the fused step kernel
+    // costs a few us of GPU time: on every step it was ~20 % of a 6x64 simulation step, on every
+    // 8th still ~10 % of a bf16 one); those steps run as separate kernels, the others through the
+    // fused step kernel
     int pending = -1;                  // step whose backup is still to launch
     for (int i = i0; i < i1; i++) {
         const bool timed = tm && i % TIMING_EVERY == 0;

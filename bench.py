@@ -372,7 +372,7 @@ def main():
                 "frac": conv_tflops / peak, "traffic": traffic,
                 "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
                 "kernel": "%s: input conv + %d residual convs + heads in one launch, %s; algorithmic FLOPs = direct-conv "
-                          "FLOPs; %d launches timed (HIP events on every 8th simulation step)"
+                          "FLOPs; %d launches timed (HIP events on every 32nd simulation step)"
                           % (kname, 2 * B, "v_mfma_f32_16x16x32_bf16" if dtype == "bf16" else "v_mfma_f32_16x16x4_f32",
                              tm["conv_launches"]),
                 "executed_tflops": exec_tflops, "executed_frac": exec_tflops / peak,
@@ -428,7 +428,7 @@ def main():
     tower_tflops = tm["tower_flop"] / (tm["tower_ms"] * 1e-3) / 1e12 if tm["tower_ms"] > 0 else 0.0
     peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
     # select_bytes covers every k_select launch of the window (steps x K); the event times cover
-    # the sampled launches (az_timing: every 8th simulation step)
+    # the sampled launches (az_timing: every 32nd simulation step)
     sel_bytes_per_launch = tm["select_bytes"] / max(args.steps * K, 1)
     sel_ms_per_launch = tm["select_ms"] / max(tm["select_launches"], 1)
     sel_gbs = sel_bytes_per_launch / (sel_ms_per_launch * 1e-3) / 1e9 if tm["select_ms"] > 0 else 0.0
