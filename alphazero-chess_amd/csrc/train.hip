@@ -219,6 +219,7 @@ colsum_kernel(const float* __restrict__ V, int ld, int C, int R, const float* __
     if (c < C) {
         const float mu = (MODE >= 1) ? mean[c] : 0.0f;
         const float sd = (MODE == 2) ? stdv[c] : 1.0f;
+#pragma unroll 4
         for (int r = rbeg + p; r < rend; r += 4) {
             const size_t e = (size_t)r * ld + c;
             if constexpr (MODE == 0) {
@@ -243,31 +244,43 @@ colsum_kernel(const float* __restrict__ V, int ld, int C, int R, const float* __
     }
 }
 
-// sum the row-block partials of channel c in order
-__device__ __forceinline__ float part_sum(const float* part, int nblk, int C, int c, int which) {
+// sum the row-block partials of channel c, one wavefront per channel: lane l adds blocks
+// l, l + 64, ... in order, then a fixed butterfly over the lanes -- a fixed order (the step stays
+// bit-reproducible), 64 loads in flight instead of one dependent chain of nblk
+__device__ __forceinline__ float part_sum(const float* part, int nblk, int C, int c, int which, int lane) {
     float s = 0.0f;
-    for (int b = 0; b < nblk; b++) s += part[((size_t)b * 2 + which) * C + c];
+    for (int b = lane; b < nblk; b += 64) s += part[((size_t)b * 2 + which) * C + c];
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
     return s;
 }
+// one wavefront per channel: launch finalize_grid(C) blocks of 256 threads
+inline int finalize_grid(int C) { return (C * 64 + 255) / 256; }
+#define FIN_CHANNEL()                                                       \
+    const int c = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);    \
+    const int lane = threadIdx.x & 63;                                      \
+    if (c >= C) return
 
 // dst[c] = sum  (bias gradients)
 __global__ void finalize_sum_kernel(const float* __restrict__ part, int nblk, int C, float* __restrict__ dst) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c < C) dst[c] = part_sum(part, nblk, C, c, 0);
+    FIN_CHANNEL();
+    const float s = part_sum(part, nblk, C, c, 0, lane);
+    if (lane == 0) dst[c] = s;
 }
 
 // mean[c] = sum / R
 __global__ void finalize_mean_kernel(const float* __restrict__ part, int nblk, int C, int R, float* __restrict__ mean) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c < C) mean[c] = part_sum(part, nblk, C, c, 0) / (float)R;
+    FIN_CHANNEL();
+    const float s = part_sum(part, nblk, C, c, 0, lane);
+    if (lane == 0) mean[c] = s / (float)R;
 }
 
 // var = sum / R; std = sqrt(var + eps); running stats: rm = rm*0.9 + mean*0.1, rv = rv*0.9 + var*0.1
 __global__ void finalize_var_kernel(const float* __restrict__ part, int nblk, int C, int R, const float* __restrict__ mean,
                                     float* __restrict__ stdv, float* __restrict__ rmean, float* __restrict__ rvar) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    const float var = part_sum(part, nblk, C, c, 0) / (float)R;
+    FIN_CHANNEL();
+    const float var = part_sum(part, nblk, C, c, 0, lane) / (float)R;
+    if (lane != 0) return;
     stdv[c] = sqrtf(var + 1e-5f);
     rmean[c] = rmean[c] * 0.9f + mean[c] * 0.1f;
     rvar[c] = rvar[c] * 0.9f + var * 0.1f;
@@ -276,11 +289,14 @@ __global__ void finalize_var_kernel(const float* __restrict__ part, int nblk, in
 // BN backward sums: dbeta[c] = sum dz, dgamma[c] = sum dz*yhat
 __global__ void finalize_bnback_kernel(const float* __restrict__ part, int nblk, int C, float* __restrict__ dgamma,
                                        float* __restrict__ dbeta) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    dbeta[c] = part_sum(part, nblk, C, c, 0);
-    dgamma[c] = part_sum(part, nblk, C, c, 1);
+    FIN_CHANNEL();
+    const float b = part_sum(part, nblk, C, c, 0, lane), g = part_sum(part, nblk, C, c, 1, lane);
+    if (lane == 0) {
+        dbeta[c] = b;
+        dgamma[c] = g;
+    }
 }
+#undef FIN_CHANNEL
 
 // ------------------------------------------------------------------ element-wise
 // out = relu(((y - mean) / std) * gamma + beta [+ res])   (burn BatchNorm::forward_shared + relu)
@@ -615,9 +631,9 @@ int bn_forward(Trainer* T, int bi, const float* Y, int ld, int C, int R, size_t 
     const int nb = nblk_rows(R);
     dim3 g(nb, (C + 63) / 64);
     tr::colsum_kernel<0><<<g, 256, 0, T->st>>>(Y, ld, C, R, nullptr, nullptr, nullptr, nullptr, T->cpart);
-    tr::finalize_mean_kernel<<<(C + 255) / 256, 256, 0, T->st>>>(T->cpart, nb, C, R, mean);
+    tr::finalize_mean_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(T->cpart, nb, C, R, mean);
     tr::colsum_kernel<1><<<g, 256, 0, T->st>>>(Y, ld, C, R, mean, nullptr, nullptr, nullptr, T->cpart);
-    tr::finalize_var_kernel<<<(C + 255) / 256, 256, 0, T->st>>>(T->cpart, nb, C, R, mean, sd, P + 2 * C, P + 3 * C);
+    tr::finalize_var_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(T->cpart, nb, C, R, mean, sd, P + 2 * C, P + 3 * C);
     tr::bn_apply_kernel<<<grid_for((size_t)R * C), 256, 0, T->st>>>(Y, ld, C, R, mean, sd, P, P + C, res, out);
     return hipGetLastError() == hipSuccess ? 0 : fail("bn forward failed");
 }
@@ -632,7 +648,7 @@ int bn_backward(Trainer* T, int bi, const float* dout, const float* O, const flo
     tr::colsum_kernel<2><<<g, 256, 0, T->st>>>(dout, ld, C, R, mean, sd, O, Y, T->cpart);
     float* dgam = T->g + bn_off;
     float* dbet = T->g + bn_off + C;
-    tr::finalize_bnback_kernel<<<(C + 255) / 256, 256, 0, T->st>>>(T->cpart, nb, C, dgam, dbet);
+    tr::finalize_bnback_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(T->cpart, nb, C, dgam, dbet);
     tr::bn_back_kernel<<<grid_for((size_t)R * C), 256, 0, T->st>>>(dout, O, Y, ld, C, R, mean, sd, T->p + bn_off, dgam,
                                                                    dbet, dy, dres);
     return hipGetLastError() == hipSuccess ? 0 : fail("bn backward failed");
@@ -642,7 +658,7 @@ int bias_grad(Trainer* T, const float* dy, int ld, int C, int R, float* dst) {
     const int nb = nblk_rows(R);
     dim3 g(nb, (C + 63) / 64);
     tr::colsum_kernel<0><<<g, 256, 0, T->st>>>(dy, ld, C, R, nullptr, nullptr, nullptr, nullptr, T->cpart);
-    tr::finalize_sum_kernel<<<(C + 255) / 256, 256, 0, T->st>>>(T->cpart, nb, C, dst);
+    tr::finalize_sum_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(T->cpart, nb, C, dst);
     return hipGetLastError() == hipSuccess ? 0 : fail("bias grad failed");
 }
 
@@ -709,7 +725,7 @@ int trainer_grads(Trainer* T, const float* planes, const float* tpol, const floa
         const int nb = nblk_rows(B);
         dim3 g(nb, 2);
         tr::colsum_kernel<0><<<g, 256, 0, st>>>(T->vpart, 65, 65, B, nullptr, nullptr, nullptr, nullptr, T->cpart);
-        tr::finalize_sum_kernel<<<1, 128, 0, st>>>(T->cpart, nb, 65, T->dwtmp);
+        tr::finalize_sum_kernel<<<tr::finalize_grid(65), 256, 0, st>>>(T->cpart, nb, 65, T->dwtmp);
         AZ_HIP(hipMemcpyAsync(T->g + L.l2w, T->dwtmp, 64 * sizeof(float), hipMemcpyDeviceToDevice, st));
         AZ_HIP(hipMemcpyAsync(T->g + L.l2b, T->dwtmp + 64, sizeof(float), hipMemcpyDeviceToDevice, st));
     }
