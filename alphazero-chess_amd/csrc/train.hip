@@ -63,22 +63,43 @@ conv_f32_kernel(const float* __restrict__ X, int ldx, int K, const float* __rest
 #pragma unroll
     for (int i = 0; i < 4; i++) acc[i][0] = acc[i][1] = f32x4{0, 0, 0, 0};
     if (tid < XS) xs[CM * XS + tid] = 0.0f;
+    // the next K chunk's X and W slices are read into registers while the current chunk's MFMAs
+    // run (software pipeline), then written to LDS after the barrier
+    constexpr int NXV = CM * (CK / 4) / 256, NWV = (TAPS * CK * (CN / 4) + 255) / 256;
+    float4 xv[NXV], wv[NWV];
+    auto fetch = [&](int k0) {
+#pragma unroll
+        for (int j = 0; j < NXV; j++) {
+            const int i = tid + j * 256, rr = i >> 2, c4 = (i & 3) * 4;
+            xv[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (r0 + rr < R) xv[j] = *reinterpret_cast<const float4*>(X + (size_t)(r0 + rr) * ldx + k0 + c4);
+        }
+#pragma unroll
+        for (int j = 0; j < NWV; j++) {
+            const int i = tid + j * 256;
+            const int t = i / (CK * CN / 4), rem = i % (CK * CN / 4), kk = rem / (CN / 4), n4 = (rem % (CN / 4)) * 4;
+            wv[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (i < TAPS * CK * (CN / 4) && n0 + n4 < N)
+                wv[j] = *reinterpret_cast<const float4*>(W + ((size_t)t * K + k0 + kk) * N + n0 + n4);
+        }
+    };
+    fetch(0);
     for (int k0 = 0; k0 < K; k0 += CK) {
         __syncthreads();
-        for (int i = tid; i < CM * (CK / 4); i += 256) {
-            const int rr = i >> 2, c4 = (i & 3) * 4;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (r0 + rr < R) v = *reinterpret_cast<const float4*>(X + (size_t)(r0 + rr) * ldx + k0 + c4);
+#pragma unroll
+        for (int j = 0; j < NXV; j++) {
+            const int i = tid + j * 256, rr = i >> 2, c4 = (i & 3) * 4;
             float* d = xs + rr * XS + c4;
-            d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+            d[0] = xv[j].x; d[1] = xv[j].y; d[2] = xv[j].z; d[3] = xv[j].w;
         }
-        for (int i = tid; i < TAPS * CK * (CN / 4); i += 256) {
+#pragma unroll
+        for (int j = 0; j < NWV; j++) {
+            const int i = tid + j * 256;
             const int t = i / (CK * CN / 4), rem = i % (CK * CN / 4), kk = rem / (CN / 4), n4 = (rem % (CN / 4)) * 4;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (n0 + n4 < N) v = *reinterpret_cast<const float4*>(W + ((size_t)t * K + k0 + kk) * N + n0 + n4);
-            *reinterpret_cast<float4*>(ws + (t * CK + kk) * WS + n4) = v;
+            if (i < TAPS * CK * (CN / 4)) *reinterpret_cast<float4*>(ws + (t * CK + kk) * WS + n4) = wv[j];
         }
         __syncthreads();
+        if (k0 + CK < K) fetch(k0 + CK);
 #pragma unroll 1
         for (int t = 0; t < TAPS; t++) {
             int aoff[4];
