@@ -169,19 +169,32 @@ wgrad_f32_kernel(const float* __restrict__ X, int ldx, int K, const float* __res
 #pragma unroll
         for (int i = 0; i < 4; i++) acc[t][i] = f32x4{0, 0, 0, 0};
     if (tid < GS) xs[GR * GS + tid] = 0.0f;
+    // software pipeline: the next GR rows of X and dY are read into registers while the current
+    // rows' MFMAs run, and written to LDS after the barrier
+    constexpr int NV = GR * 16 / 256;
+    float4 xv[NV], dv[NV];
+    auto fetch = [&](int rc) {
+#pragma unroll
+        for (int j = 0; j < NV; j++) {
+            const int i = tid + j * 256, rr = i >> 4, c4 = (i & 15) * 4;
+            xv[j] = dv[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (rc + rr < rend) {
+                if (k0 + c4 < K) xv[j] = *reinterpret_cast<const float4*>(X + (size_t)(rc + rr) * ldx + k0 + c4);
+                if (n0 + c4 < N) dv[j] = *reinterpret_cast<const float4*>(DY + (size_t)(rc + rr) * ldd + n0 + c4);
+            }
+        }
+    };
+    if (rbeg < rend) fetch(rbeg);
     for (int rc = rbeg; rc < rend; rc += GR) {
         __syncthreads();
-        for (int i = tid; i < GR * 16; i += 256) {
-            const int rr = i >> 4, c4 = (i & 15) * 4;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f), d = v;
-            if (rc + rr < rend) {
-                if (k0 + c4 < K) v = *reinterpret_cast<const float4*>(X + (size_t)(rc + rr) * ldx + k0 + c4);
-                if (n0 + c4 < N) d = *reinterpret_cast<const float4*>(DY + (size_t)(rc + rr) * ldd + n0 + c4);
-            }
-            *reinterpret_cast<float4*>(xs + rr * GS + c4) = v;
-            *reinterpret_cast<float4*>(ds + rr * GS + c4) = d;
+#pragma unroll
+        for (int j = 0; j < NV; j++) {
+            const int i = tid + j * 256, rr = i >> 4, c4 = (i & 15) * 4;
+            *reinterpret_cast<float4*>(xs + rr * GS + c4) = xv[j];
+            *reinterpret_cast<float4*>(ds + rr * GS + c4) = dv[j];
         }
         __syncthreads();
+        if (rc + GR < rend) fetch(rc + GR);
 #pragma unroll 2
         for (int q = 0; q < GR / 4; q++) {
             const int rq = q * 4 + (lane >> 4);
