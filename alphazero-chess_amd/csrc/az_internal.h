@@ -193,6 +193,10 @@ int net_planes_from_host_layout(NetDev* n, const float* d_in, int rows, void* pl
 // fused tower (tower.hip): input conv + residual tower + heads in one launch (bf16 and f32).
 bool tower_supported(const NetDev* n);
 bool wino_supported(const NetDev* n);   // f32, F >= 64, Winograd weights built: tower32w_kernel
+// persistent per-game simulation kernel (tower.hip, k_sims32w): simulation steps [step0, step1) of
+// every game, tree steps and Winograd evaluations in one workgroup per game, all backed up at the end
+bool sims_persistent_supported(const NetDev* n);
+int sims_persistent(const NetDev* n, const Engine& E, const SearchOut& so, int step0, int step1, hipStream_t st);
 int tower_forward(NetDev* n, const void* planes, const int* count, int rows, float* pol, float* val,
                   const SearchOut* so, hipStream_t st);
 size_t act_bytes(int dtype);

@@ -16,6 +16,7 @@
 #include <string.h>
 
 #include "az_internal.h"
+#include "search_dev.h"
 
 #ifndef AZ_TOWER_WB256
 #define AZ_TOWER_WB256 1   // F=256: 8 waves x 2 boards (WB=2, 16 waves, measured 10% slower: spills)
@@ -1065,7 +1066,13 @@ tower32_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __rest
 #ifndef AZ_WINO_TSPLIT
 #define AZ_WINO_TSPLIT 8   // steps between the patch reads and their transform + V writes
 #endif
-constexpr int WINO_TLOAD = AZ_WINO_TLOAD, WINO_TSPLIT = AZ_WINO_TSPLIT;
+#ifndef AZ_WINO_TSTAG
+#define AZ_WINO_TSTAG 0    // steps by which the second wave of each SIMD pair (w >= NWV / 2) delays its transform
+#endif
+#ifndef AZ_WINO_TADDR
+#define AZ_WINO_TADDR 1    // 1: patch addresses as per-column bases + immediate row offsets (no per-element multiply)
+#endif
+constexpr int WINO_TLOAD = AZ_WINO_TLOAD, WINO_TSPLIT = AZ_WINO_TSPLIT, WINO_TSTAG = AZ_WINO_TSTAG;
 constexpr int WINO_PF = AZ_WINO_PF;
 constexpr int WINO_LA = AZ_WINO_LA;
 #ifndef AZ_WINO_NWV
@@ -1152,6 +1159,30 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase, in
         // patch addresses recomputed per chunk from a laundered index: hoisted out of the chunk
         // loop they were 16 loop-invariant registers, and spilled
         const int tl = vgpr_index(ttx);
+#if AZ_WINO_TADDR
+        // element (i, j) of the patch is square (2 tty - 1 + i, 2 tl - 1 + j): the row part is
+        // wave-uniform (tty = w & 3), so every address is a per-column lane base + a row offset
+        // that is an instruction immediate (rows 1, 2) or one scalar add (rows 0, 3, clamped onto
+        // the board when they fall off it); off-board elements are read at the clamped square and
+        // zeroed afterwards (row: wave-uniform select, column: lane select)
+        constexpr int R16 = RS * 16;
+        const int rowb1 = (2 * tty) * 8 * R16;                              // row i = 1
+        const int d0 = tty > 0 ? -8 * R16 : 0, d3 = tty < 3 ? 16 * R16 : 8 * R16;
+        const bool c0ok = tl > 0, c3ok = tl < 3;
+        const int cs0 = c0ok ? 2 * tl - 1 : 0, cs3 = c3ok ? 2 * tl + 2 : 7;
+#pragma unroll
+        for (int it = 0; it < IT; it++) {
+            const int chan = (c * CH + tchan(it)) * 4 + rowb1;
+            const int cb[4] = {cs0 * R16 + chan, 2 * tl * R16 + chan, (2 * tl + 1) * R16 + chan, cs3 * R16 + chan};
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                d[it][0][j] = *reinterpret_cast<const float*>(ldsb + cb[j] + d0);
+                d[it][1][j] = *reinterpret_cast<const float*>(ldsb + cb[j]);
+                d[it][2][j] = *reinterpret_cast<const float*>(ldsb + cb[j] + 8 * R16);
+                d[it][3][j] = *reinterpret_cast<const float*>(ldsb + cb[j] + d3);
+            }
+        }
+#else
         const int pty = 2 * tty - 1, ptx = 2 * tl - 1;
 #pragma unroll
         for (int it = 0; it < IT; it++) {
@@ -1165,17 +1196,33 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase, in
                     d[it][i][j] = *reinterpret_cast<const float*>(ldsb + (ok ? (py * 8 + px) * RS * 16 : zero_off) + chan);
                 }
         }
+#endif
     };
     auto tstore = [&](int buf, const float (&d)[IT][4][4]) {
+#if AZ_WINO_TADDR
+        const int tl = vgpr_index(ttx);
+#endif
 #pragma unroll
         for (int it = 0; it < IT; it++) {
+            float e[4][4];
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    e[i][j] = d[it][i][j];
+#if AZ_WINO_TADDR   // zero the off-board elements tload read at clamped squares
+                    if ((i == 0 && tty == 0) || (i == 3 && tty == 3)) e[i][j] = 0.f;
+                    if (j == 0) e[i][j] = tl > 0 ? e[i][j] : 0.f;
+                    if (j == 3) e[i][j] = tl < 3 ? e[i][j] : 0.f;
+#endif
+                }
             float t[4][4];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                t[0][j] = d[it][0][j] - d[it][2][j];
-                t[1][j] = d[it][1][j] + d[it][2][j];
-                t[2][j] = d[it][2][j] - d[it][1][j];
-                t[3][j] = d[it][1][j] - d[it][3][j];
+                t[0][j] = e[0][j] - e[2][j];
+                t[1][j] = e[1][j] + e[2][j];
+                t[2][j] = e[2][j] - e[1][j];
+                t[3][j] = e[1][j] - e[3][j];
             }
             char* vb = ldsb + vbase + buf * VBYTES + vwr(tchan(it));
 #pragma unroll
@@ -1281,8 +1328,20 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase, in
             if (c == 3 && (st & 7) == 7) WT_STAMP(20 + (st >> 3));   // chunk 3, after steps 7, 15, 23, 31
 #endif
 #ifndef AZ_WINO_NOTRANSFORM   // experiment only: no input transforms inside the chunk loop (wrong results)
-            if (st == WINO_TLOAD / XS && more) tload(c + 1, dn);
-            if (st == (WINO_TLOAD + WINO_TSPLIT) / XS && more) tstore((c + 1) & 1, dn);
+            // (a stagger that would not fit in this F's chunk is dropped)
+            constexpr int TSG = (WINO_TLOAD + WINO_TSTAG + WINO_TSPLIT) / XS < SPX ? WINO_TSTAG : 0;
+            if constexpr (TSG == 0) {
+                if (st == WINO_TLOAD / XS && more) tload(c + 1, dn);
+                if (st == (WINO_TLOAD + WINO_TSPLIT) / XS && more) tstore((c + 1) & 1, dn);
+            } else {
+                // the two waves of a SIMD pair run their transform VALU blocks at different steps,
+                // so that one of them keeps the matrix pipe busy
+                const bool late = w >= NWV / 2;
+                if (st == WINO_TLOAD / XS && more && !late) tload(c + 1, dn);
+                if (st == (WINO_TLOAD + TSG) / XS && more && late) tload(c + 1, dn);
+                if (st == (WINO_TLOAD + WINO_TSPLIT) / XS && more && !late) tstore((c + 1) & 1, dn);
+                if (st == (WINO_TLOAD + TSG + WINO_TSPLIT) / XS && more && late) tstore((c + 1) & 1, dn);
+            }
 #endif
         }
         WT_STAMP(2 + 2 * c);
@@ -1372,10 +1431,11 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase, in
 #undef WT_STAMP
 }
 
+// one board (batch row row0) through the Winograd f32 tower, all NWV waves of the workgroup
 template <int F, bool SEARCH>
-__global__ void __launch_bounds__(WinoCfg<F>::NWV * 64)
-tower32w_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __restrict__ count_ptr, int rows,
-                float* __restrict__ pol_out, float* __restrict__ val_out, SearchOut so) {
+__device__ __forceinline__ void tower32w_board(const float* __restrict__ planes, const TowerArgs& ta, int row0,
+                                               float* __restrict__ pol_out, float* __restrict__ val_out,
+                                               const SearchOut& so, int tid) {
     constexpr int NWV = WinoCfg<F>::NWV, NT = NWV * 64, NN = WinoCfg<F>::NN, XS = WinoCfg<F>::XS;
     constexpr int XH = WinoCfg<F>::XH, NCW = NWV / XH;    // waves of the direct input conv
     constexpr int RSF = F / 4 + 2, RSI = 32 / 4 + 2;
@@ -1386,10 +1446,7 @@ tower32w_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __res
     static_assert(HeadsScratch<1, NT, heads_npart(NT, true)>::FLOATS * 4 <= VSZ * 16, "heads scratch must fit in V");
     static_assert(64 * RSI <= VSZ, "input planes must fit in V");
     __shared__ __attribute__((aligned(16))) uint4 lds[XSZ + VSZ + ZN];
-    const int count = count_ptr ? min(load_fresh(count_ptr), rows) : rows;
-    const int row0 = blockIdx.x;
-    if (row0 >= count) return;
-    const int tid = threadIdx.x, lane = tid & 63;
+    const int lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     uint4* X = lds;
     uint4* V = lds + XSZ;
@@ -1476,6 +1533,87 @@ tower32w_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __res
 #undef WC_STAMP
 }
 
+template <int F, bool SEARCH>
+__global__ void __launch_bounds__(WinoCfg<F>::NWV * 64)
+tower32w_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __restrict__ count_ptr, int rows,
+                float* __restrict__ pol_out, float* __restrict__ val_out, SearchOut so) {
+    const int count = count_ptr ? min(load_fresh(count_ptr), rows) : rows;
+    if ((int)blockIdx.x >= count) return;
+    tower32w_board<F, SEARCH>(planes, ta, blockIdx.x, pol_out, val_out, so, threadIdx.x);
+}
+
+// k_sims32w: simulation steps [step0, step1) of one game per workgroup, with no grid-wide step
+// boundary.  A game's simulations only touch its own tree (tree.rs:180-207 runs them one after
+// the other per game), so the workgroup of game g loops: wave 0 backs up the previous
+// simulation, selects and expands (search_dev.h, the same functions as k_step); if the leaf
+// needs the network, all waves evaluate it through the Winograd tower as batch row g, whose
+// heads write the priors into the new node's edges and the value into value[g].  The last
+// simulation is backed up before the kernel ends.  It replaces 2 launches per simulation step
+// (k_step + the tower, each step waiting for the slowest game of both) when every game has a
+// CU of its own (G <= CUs: C2), and is bit-identical to them (tests/test_gpu_search.py).
+// Cross-wave hand-offs: the workgroup barriers carry workgroup-scope fences; every record written
+// inside the kernel is read back through vector loads (vgpr_index), never the scalar cache.
+template <int F>
+__global__ void __launch_bounds__(WinoCfg<F>::NWV * 64)
+k_sims32w(Engine E, TowerArgs ta, SearchOut so, int step0, int step1) {
+    __shared__ int s_kind;
+    if (!E.active[vgpr_index(blockIdx.x)]) return;     // constant within a move
+#ifdef AZ_SIMS_TRACE   // experiment: per-game cycles in the tree phase / the tower phase (tools/sims_trace.py)
+    unsigned long long c_tree = 0, c_tower = 0, n_eval = 0, t0 = __builtin_amdgcn_s_memtime(), t1 = t0;
+#endif
+    for (int step = step0; step <= step1; step++) {
+        // indices laundered per simulation so that neither phase's loop-invariant address
+        // arithmetic is hoisted across the other (it would stay live through it and spill)
+        const int tid = vgpr_index(threadIdx.x), g = vgpr_index(blockIdx.x);
+        const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+        if (w == 0) {
+            if (step > step0) {                        // the previous simulation's backup
+                backup_game(E, g, lane);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            }
+            int kind = X_NONE, nid = -1;
+            if (step < step1) {
+                select_game(E, g, lane);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                kind = expand_leaf_wave(E, g, lane, &nid, step);
+                if (lane == 0) {
+                    if (kind == X_ROW) {
+                        E.row_game[g] = g;
+                        E.row_node[g] = nid;
+                        E.leaf_row[g] = g;
+                        atomicAdd(&E.batch_hist[step], 1);
+                        atomicAdd(&E.ctr->evals, 1ull);
+                    } else if (kind == X_TERMINAL) {
+                        atomicAdd(&E.ctr->terminal, 1ull);
+                    } else if (kind == X_CACHED) {
+                        atomicAdd(&E.ctr->cache_hits, 1ull);
+                    }
+                }
+            }
+            if (lane == 0) s_kind = kind;
+        }
+        __syncthreads();
+        const int kind = s_kind;
+#ifdef AZ_SIMS_TRACE
+        t1 = __builtin_amdgcn_s_memtime();
+        c_tree += t1 - t0;
+#endif
+        if (kind == X_ROW) tower32w_board<F, true>(nullptr, ta, g, nullptr, nullptr, so, tid);
+        __syncthreads();
+#ifdef AZ_SIMS_TRACE
+        t0 = __builtin_amdgcn_s_memtime();
+        c_tower += t0 - t1;
+        n_eval += kind == X_ROW;
+#endif
+    }
+#ifdef AZ_SIMS_TRACE
+    if (threadIdx.x == 0) {
+        unsigned long long* tr = E.trace + (size_t)vgpr_index(blockIdx.x) * 16;
+        tr[8] += c_tree; tr[9] += c_tower; tr[10] += n_eval; tr[11] += (unsigned long long)(step1 - step0 + 1);
+    }
+#endif
+}
+
 bool tower_supported(const NetDev* n) {
     return (n->dtype == AZ_DTYPE_BF16 || n->dtype == AZ_DTYPE_F32) && n->blocks <= 40 &&
            (n->filters == 256 || n->filters == 128 || n->filters == 64 || n->filters == 32);
@@ -1485,27 +1623,49 @@ bool wino_supported(const NetDev* n) {
     return n->dtype == AZ_DTYPE_F32 && n->winograd && n->filters >= 64 && (int)n->wino_w.size() == 2 * n->blocks;
 }
 
-int tower_forward(NetDev* n, const void* planes, const int* count, int rows, float* pol, float* val,
-                  const SearchOut* so, hipStream_t st) {
-    if (rows <= 0) return 0;
-    if (!tower_supported(n)) return fail("fused tower: unsupported net");
-    if (!planes && (!so || !so->npos)) return fail("fused tower: no planes and no leaf positions to encode");
+static TowerArgs tower_args(const NetDev* n) {
     TowerArgs ta;
     memset(&ta, 0, sizeof(ta));
     for (int i = 0; i < 1 + 2 * n->blocks; i++) {
-        const int src = i;
-        ta.w[i] = reinterpret_cast<const uint4*>(n->conv_w[src]);
-        ta.b[i] = n->conv_b[src];
+        ta.w[i] = reinterpret_cast<const uint4*>(n->conv_w[i]);
+        ta.b[i] = n->conv_b[i];
+        ta.wbytes[i] = (unsigned)n->conv_bytes[i];
     }
     ta.head = n->head;
     ta.head_frag = reinterpret_cast<const uint4*>(n->head_frag);
     ta.head_frag32 = reinterpret_cast<const uint4*>(n->head_frag32);
-    for (int i = 0; i < 1 + 2 * n->blocks; i++) ta.wbytes[i] = (unsigned)n->conv_bytes[i];
     for (size_t i = 0; i < n->wino_w.size(); i++) {
         ta.ww[i] = reinterpret_cast<const uint4*>(n->wino_w[i]);
         ta.wwbytes[i] = (unsigned)n->wino_bytes[i];
     }
     ta.blocks = n->blocks;
+    return ta;
+}
+
+bool sims_persistent_supported(const NetDev* n) { return tower_supported(n) && wino_supported(n); }
+
+// simulation steps [step0, step1) of every game through k_sims32w (one workgroup per game);
+// ends with every simulation backed up
+int sims_persistent(const NetDev* n, const Engine& E, const SearchOut& so, int step0, int step1, hipStream_t st) {
+    if (step1 <= step0) return 0;
+    if (!sims_persistent_supported(n)) return fail("persistent simulation kernel: needs the f32 Winograd tower");
+    const TowerArgs ta = tower_args(n);
+#define AZ_SIMS32W(FF)                                                                                  \
+    if (n->filters == FF) {                                                                            \
+        k_sims32w<FF><<<E.G, WinoCfg<FF>::NWV * 64, 0, st>>>(E, ta, so, step0, step1);                 \
+        return hipGetLastError() == hipSuccess ? 0 : fail("persistent simulation kernel launch failed"); \
+    }
+    AZ_SIMS32W(256) AZ_SIMS32W(128) AZ_SIMS32W(64)
+#undef AZ_SIMS32W
+    return fail("persistent simulation kernel: unsupported filters");
+}
+
+int tower_forward(NetDev* n, const void* planes, const int* count, int rows, float* pol, float* val,
+                  const SearchOut* so, hipStream_t st) {
+    if (rows <= 0) return 0;
+    if (!tower_supported(n)) return fail("fused tower: unsupported net");
+    if (!planes && (!so || !so->npos)) return fail("fused tower: no planes and no leaf positions to encode");
+    TowerArgs ta = tower_args(n);
 #if defined(AZ_TOWER_TRACE) || defined(AZ_WINO_TRACE)
 #ifndef AZ_TOWER_TRACE
 #define AZ_TOWER_TRACE AZ_WINO_TRACE

@@ -194,3 +194,33 @@ def test_fused_step_kernel_matches_separate_kernels(require_gpu, monkeypatch, ca
                             for s in sp.drain())))
     assert runs[0][0][0] == 12 * 40 * 6
     assert runs[0] == runs[1] == runs[2]
+
+
+@pytest.mark.parametrize("timing", [False, True])
+def test_persistent_sims_match_step_kernels(require_gpu, monkeypatch, timing):
+    """k_sims32w (each game's simulation loop in one workgroup: backup, select, expand and the
+    Winograd f32 evaluation, no grid-wide step boundary) against k_step + the batched tower, and
+    against the timed mix (every 32nd simulation step through the separate kernels): identical
+    visit counts, improved policies and depths of one search, identical simulation / evaluation /
+    terminal-leaf counts over several self-play moves."""
+    net = A.AlphaZero(6, 64, weights=A.random_weights(6, 64, seed=42), dtype="f32")
+    runs = []
+    for persist in ("1", "0"):
+        monkeypatch.setenv("AZ_PERSIST", persist)
+        s = A.BatchedSearch(net, games=24, sims=300, seed=29, cache_capacity=0)
+        s.timing(reset=True, enable=timing)
+        s.set_roots([[]] * 12 + [[588]] * 12, apply_noise=True)
+        imp, vis, dep = s.run()
+        st = s.stats()
+        sp = A.SelfPlay(net, games=24, sims=72, seed=31, cache_capacity=0)
+        sp.reset()
+        sp.search.timing(reset=True, enable=timing)
+        for _ in range(5):
+            sp.step()
+        st2 = sp.search.stats()
+        runs.append((imp, vis, dep, (st["sims"], st["evals"], st["terminal_leaves"], st["overflow"]),
+                     (st2["sims"], st2["evals"], st2["terminal_leaves"], st2["overflow"])))
+    (i1, v1, d1, a1, b1), (i0, v0, d0, a0, b0) = runs
+    assert a1[0] == 24 * 300 and a1[3] == 0 and b1[0] == 24 * 72 * 5 and b1[3] == 0
+    assert np.array_equal(v1, v0) and np.array_equal(i1, i0) and np.array_equal(d1, d0)
+    assert a1 == a0 and b1 == b0
