@@ -1067,7 +1067,7 @@ tower32_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __rest
 #define AZ_WINO_TSPLIT 8   // steps between the patch reads and their transform + V writes
 #endif
 #ifndef AZ_WINO_TSTAG
-#define AZ_WINO_TSTAG 0    // steps by which the second wave of each SIMD pair (w >= NWV / 2) delays its transform
+#define AZ_WINO_TSTAG 16   // steps by which the second wave of each SIMD pair (w >= NWV / 2) delays its transform
 #endif
 #ifndef AZ_WINO_TADDR
 #define AZ_WINO_TADDR 1    // 1: patch addresses as per-column bases + immediate row offsets (no per-element multiply)
@@ -1077,6 +1077,12 @@ constexpr int WINO_PF = AZ_WINO_PF;
 constexpr int WINO_LA = AZ_WINO_LA;
 #ifndef AZ_WINO_NWV
 #define AZ_WINO_NWV 8
+#endif
+#ifndef AZ_WINO_SYNC
+#define AZ_WINO_SYNC 0     // experiment: a workgroup barrier every N steps of a chunk (0: only the per-chunk barrier)
+#endif
+#ifndef AZ_WINO_PRIO2
+#define AZ_WINO_PRIO2 0    // experiment: progress-based issue priority between the two waves of a SIMD
 #endif
 
 
@@ -1259,6 +1265,10 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase, in
     }
     __syncthreads();
     WT_STAMP(1);
+#if AZ_WINO_PRIO2
+    __shared__ int prog[NWV];
+    int prog_other = 0;
+#endif
 #pragma unroll 1
     for (int c = 0; c < NCHUNK; c++) {
         float dn[IT][4][4];
@@ -1326,6 +1336,19 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase, in
             __builtin_amdgcn_sched_barrier(0);
 #ifdef AZ_WINO_TRACE
             if (c == 3 && (st & 7) == 7) WT_STAMP(20 + (st >> 3));   // chunk 3, after steps 7, 15, 23, 31
+#endif
+#if AZ_WINO_SYNC > 0   // experiment: extra workgroup barriers inside a chunk (bounds the skew of a SIMD's two waves)
+            if ((st + 1) % AZ_WINO_SYNC == 0 && st + 1 < SPX) __syncthreads();
+#endif
+#if AZ_WINO_PRIO2   // experiment: every 4 steps the wave behind its SIMD partner (w ^ NWV/2) takes issue priority
+            if ((st & 3) == 3) {
+                // the partner's progress was read at the previous check (its latency is long past)
+                const int mine = c * SPX + st, other = __builtin_amdgcn_readfirstlane(prog_other);
+                if (other < mine) __builtin_amdgcn_s_setprio(0);
+                else __builtin_amdgcn_s_setprio(1);
+                prog[w] = mine;
+                prog_other = prog[w ^ (NWV / 2)];
+            }
 #endif
 #ifndef AZ_WINO_NOTRANSFORM   // experiment only: no input transforms inside the chunk loop (wrong results)
             // (a stagger that would not fit in this F's chunk is dropped)

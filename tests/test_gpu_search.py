@@ -224,3 +224,21 @@ def test_persistent_sims_match_step_kernels(require_gpu, monkeypatch, timing):
     assert a1[0] == 24 * 300 and a1[3] == 0 and b1[0] == 24 * 72 * 5 and b1[3] == 0
     assert np.array_equal(v1, v0) and np.array_equal(i1, i0) and np.array_equal(d1, d0)
     assert a1 == a0 and b1 == b0
+
+
+def test_selfplay_matches_committed_search_golden(require_gpu):
+    """C1 (BASELINE.json configs[0]: 16 simulations per move) on the GPU against the committed
+    golden vectors (tests/golden/search_c1.npz, synthetic evaluator, 2 whole games): every
+    EpisodeStep's action, depth, result, final value and root visit counts bit-exact."""
+    import os
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "search_c1.npz"))
+    _, steps = A.run_all_episodes(None, games=2, sims=16, seed=5)
+    steps = sorted(steps, key=lambda s: (s.game_id, s.ply))
+    assert len(steps) == len(g["synth_ply"])
+    off = g["synth_vis_off"]
+    for i, s in enumerate(steps):
+        assert (s.game_id, s.ply, s.action, s.search_depth, s.result) == \
+               tuple(int(g["synth_" + k][i]) for k in ("game", "ply", "action", "depth", "result")), i
+        assert np.float32(s.final_value) == g["synth_final_value"][i], i
+        ref = {int(k): float(v) for k, v in zip(g["synth_vis_idx"][off[i]:off[i + 1]], g["synth_vis_n"][off[i]:off[i + 1]])}
+        assert s.visits == ref, i
