@@ -99,6 +99,7 @@ SIGNATURES = [
     ("az_selfplay_run_sims", C.c_int, [C.c_void_p, C.c_int, P(C.c_int), P(C.c_int), P(C.c_int)]),
     ("az_selfplay_drain", C.c_int, [C.c_void_p, P(AzEpisodeStep), C.c_int]),
     ("az_search_stats_get", C.c_int, [C.c_void_p, P(AzSearchStats)]),
+    ("az_search_persistent", C.c_int, [C.c_void_p]),
     ("az_search_eval_log", C.c_int, [C.c_void_p, P(C.c_int64), P(C.c_int64), P(C.c_uint64), P(C.c_float),
                                      P(C.c_int32), P(C.c_int32), P(C.c_float)]),
     ("az_search_timing", C.c_int, [C.c_void_p, P(AzTiming), C.c_int, C.c_int]),

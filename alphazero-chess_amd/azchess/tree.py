@@ -64,6 +64,11 @@ class BatchedSearch:
         L.check(L.lib.az_search_advance(self._h, L.i32ptr(a), 1 if apply_noise else 0, L.i32ptr(res)))
         return res
 
+    @property
+    def persistent(self):
+        """True if the untimed simulation steps run through the persistent per-game kernel."""
+        return bool(L.lib.az_search_persistent(self._h))
+
     def stats(self):
         s = L.AzSearchStats()
         L.check(L.lib.az_search_stats_get(self._h, C.byref(s)))

@@ -1052,6 +1052,8 @@ int az_selfplay_drain(az_search* s, az_episode_step* out, int cap) {
     return n;
 }
 
+int az_search_persistent(az_search* s) { return s && use_persistent(s) ? 1 : 0; }
+
 int az_search_stats_get(az_search* s, az_search_stats* out) {
     if (!s || !out) return fail("null argument");
     AZ_HIP(hipSetDevice(s->device));

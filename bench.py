@@ -346,6 +346,7 @@ def main():
         barrier()
         elapsed = time.perf_counter() - t0
         tm = sp.search.timing(reset=False, enable=False)
+        tm["persistent"] = bool(getattr(sp.search, "persistent", False))
         st1 = sp.search.stats()
         c = [st1[k] - st0[k] for k in ("sims", "evals", "terminal_leaves", "moves", "max_depth_sum", "cache_hits")]
         assert c[0] == G * K * steps, (c[0], G * K * steps)
@@ -466,6 +467,11 @@ def main():
                       "avg_ms_per_launch": tm["select_ms"] / max(tm["select_launches"], 1)},
         "sim_step_ms": {k: tm[k + "_ms"] / max(tm["sim_steps"], 1)
                         for k in ("select", "expand", "encode", "tower", "heads", "backup")},
+        "sim_kernels": ("k_sims32w<%d> for the untimed simulation steps: one workgroup per game runs its backup, "
+                        "select, expand and Winograd f32 evaluation with no grid-wide step boundary (the timed "
+                        "every-32nd steps, which carry the roofline / tree_walk events, run as separate kernels)"
+                        % args.filters) if tm.get("persistent") else
+                       "k_step (backup + select + expand) + the fused tower, two launches per simulation step",
         "evals_per_sim": evals_all / max(sims_all, 1),
         "terminal_leaf_frac": term_all / max(sims_all, 1),
         "with_fen_cache": cache_res,

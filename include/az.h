@@ -179,6 +179,12 @@ typedef struct {
     int64_t node_cap, edge_cap;/* the per-game arena sizes */
 } az_search_stats;
 int az_search_stats_get(az_search* s, az_search_stats* out);
+/* 1 if the untimed simulation steps run through the persistent per-game kernel (k_sims32w: a
+ * game's backup / select / expand and its Winograd f32 evaluation in one workgroup, no grid-wide
+ * step boundary; chosen when the games fit the device in one round, the net is f32 Winograd and
+ * the FEN cache is off; env AZ_PERSIST=0/1 forces it), 0 if they run as k_step + the batched
+ * tower.  Either way the results are identical (tests/test_gpu_search.py). */
+int az_search_persistent(az_search* s);
 
 /* Evaluation log (cfg.record_evals): keys[n] (fen keys), values[n], CSR priors at the
  * legal move indices. Pass NULL arrays to query sizes. */
@@ -186,7 +192,7 @@ int az_search_eval_log(az_search* s, int64_t* n_rows, int64_t* n_priors, uint64_
                        int32_t* off, int32_t* idx, float* priors);
 
 /* Profiling: device times measured with HIP events on the engine stream while enabled, on
- * every 8th simulation step (steps 0, 8, 16, ...; every field except select_bytes covers
+ * every 32nd simulation step (steps 0, 32, 64, ...; every field except select_bytes covers
  * those sampled steps only: sim_steps = sampled steps = select_launches).
  * conv_*: the first residual 3x3 FxF conv of every simulation step (the dominant kernel);
  * conv_flop = algorithmic FLOPs of those launches (rows * 2*64*9*F*F).  tower_*: the whole
