@@ -494,7 +494,7 @@ struct az_search {
     bool timing = false;
     bool fused_steps = AZ_FUSED_STEPS != 0;   // k_step (backup + select + expand in one launch); env AZ_FUSED_STEPS=0: separate kernels
     int persist = -1;                // k_sims32w (a game's whole simulation loop in one workgroup): -1 auto
-                                     // (f32 Winograd net, FEN cache off, G <= CUs), 0 off, 1 on; env AZ_PERSIST
+                                     // (f32 Winograd or bf16 64-filter net, FEN cache off, G <= CUs), 0 off, 1 on; env AZ_PERSIST
     int cus = 256;                   // compute units of the device
     std::vector<hipEvent_t> ev;      // 7 per sim step
     az_timing acc{};

@@ -663,10 +663,11 @@ __device__ __forceinline__ void heads_group(const char* __restrict__ xb, float* 
 }
 #undef HT_STAMP
 
+// boards [row0, row0 + nb) through the bf16 tower, all waves of the workgroup
 template <int F, bool SEARCH>
-__global__ void __launch_bounds__((F / (16 * TowerCfg<F>::NCO)) * TowerCfg<F>::WB * 64)
-tower_kernel(const __bf16* __restrict__ planes, TowerArgs ta, const int* __restrict__ count_ptr, int rows,
-             float* __restrict__ pol_out, float* __restrict__ val_out, SearchOut so) {
+__device__ __forceinline__ void tower_board(const __bf16* __restrict__ planes, const TowerArgs& ta, int row0, int nb,
+                                            float* __restrict__ pol_out, float* __restrict__ val_out,
+                                            const SearchOut& so, int tid) {
     constexpr int BPB = TowerCfg<F>::BPB, WB = TowerCfg<F>::WB, BPW = BPB / WB, NCO = TowerCfg<F>::NCO;
     constexpr int NCW = F / (16 * NCO);
     constexpr int NT = NCW * WB * 64;
@@ -679,11 +680,7 @@ tower_kernel(const __bf16* __restrict__ planes, TowerArgs ta, const int* __restr
     // chunk-group split + per-wave done flags (no barrier between residual convs): F = 256 only
     constexpr int NSP = (AZ_TOWER_FLAGS && F == 256 && WB == 1) ? 2 : 1;
     __shared__ __attribute__((aligned(16))) uint4 lds[XSZ + HSZ + ZN + 6];
-    const int count = count_ptr ? min(load_fresh(count_ptr), rows) : rows;
-    const int row0 = blockIdx.x * BPB;
-    if (row0 >= count) return;
-    const int nb = min(BPB, count - row0);
-    const int tid = threadIdx.x, lane = tid & 63;
+    const int lane = tid & 63;
     TR_STAMP(0);
 #ifdef AZ_TOWER_TRACE
     if (tid == 0) ta.trace[(size_t)blockIdx.x * TR_SLOTS + 112] = __builtin_amdgcn_s_memtime();
@@ -807,6 +804,17 @@ tower_kernel(const __bf16* __restrict__ planes, TowerArgs ta, const int* __restr
 #ifdef AZ_TOWER_TRACE
     if (tid == 0) ta.trace[(size_t)blockIdx.x * TR_SLOTS + 113] = __builtin_amdgcn_s_memtime();
 #endif
+}
+
+template <int F, bool SEARCH>
+__global__ void __launch_bounds__((F / (16 * TowerCfg<F>::NCO)) * TowerCfg<F>::WB * 64)
+tower_kernel(const __bf16* __restrict__ planes, TowerArgs ta, const int* __restrict__ count_ptr, int rows,
+             float* __restrict__ pol_out, float* __restrict__ val_out, SearchOut so) {
+    constexpr int BPB = TowerCfg<F>::BPB;
+    const int count = count_ptr ? min(load_fresh(count_ptr), rows) : rows;
+    const int row0 = blockIdx.x * BPB;
+    if (row0 >= count) return;
+    tower_board<F, SEARCH>(planes, ta, row0, min(BPB, count - row0), pol_out, val_out, so, threadIdx.x);
 }
 
 // ====================================================================== f32 tower
@@ -1106,15 +1114,18 @@ template <int F> struct WinoCfg;
 #ifndef AZ_WINO64_PF
 #define AZ_WINO64_PF 2
 #endif
+#ifndef AZ_WINO64_CH
+#define AZ_WINO64_CH 64    // input channels per transform chunk at F = 64 (64: the whole input in one chunk, C2 A/B -8 %)
+#endif
 #ifndef AZ_WINO64_XH
-#define AZ_WINO64_XH 2
+#define AZ_WINO64_XH 1     // 1: 4 waves of one point set (with the single 64-channel chunk: C2 tower 102 -> 98.7 us); 2: 8 waves in point halves
 #endif
 template <> struct WinoCfg<256> {
     static constexpr int NWV = AZ_WINO_NWV, NN = 16 / NWV, XH = 1, XS = 1, CH = 32, PF = WINO_PF;
 };
 template <> struct WinoCfg<128> { static constexpr int NWV = 8, NN = 1, XH = 1, XS = 2, CH = 32, PF = WINO_PF; };
 template <> struct WinoCfg<64> {
-    static constexpr int XH = AZ_WINO64_XH, NWV = 4 * XH, NN = 1, XS = 2, CH = 32, PF = AZ_WINO64_PF;
+    static constexpr int XH = AZ_WINO64_XH, NWV = 4 * XH, NN = 1, XS = 2, CH = AZ_WINO64_CH, PF = AZ_WINO64_PF;
 };
 // Winograd weight fragment offsets: wave w's lane base (output fragments NN cw.., its point half) and
 // the byte offset of ring step t (16-channel group kl = t / NXI, point t % NXI of the half) of chunk cg
@@ -1481,7 +1492,8 @@ __device__ __forceinline__ void tower32w_board(const float* __restrict__ planes,
     constexpr int XH = WinoCfg<F>::XH, NCW = NWV / XH;    // waves of the direct input conv
     constexpr int RSF = F / 4 + 2, RSI = 32 / 4 + 2;
     constexpr int XSZ = 64 * RSF;                        // ACT, uint4 slots
-    constexpr int VSZ = 2 * WinoCfg<F>::CH * 1024 / 16;  // both V buffers (also planes staging, heads scratch)
+    // both V buffers (one when a single chunk covers the input), also planes staging / heads scratch
+    constexpr int VSZ = (F / WinoCfg<F>::CH > 1 ? 2 : 1) * WinoCfg<F>::CH * 1024 / 16;
     constexpr int PF = WinoCfg<F>::PF;
     constexpr int ZN = 16 + F / 4;
     static_assert(HeadsScratch<1, NT, heads_npart(NT, true)>::FLOATS * 4 <= VSZ * 16, "heads scratch must fit in V");
@@ -1594,8 +1606,14 @@ tower32w_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __res
 // CU of its own (G <= CUs: C2), and is bit-identical to them (tests/test_gpu_search.py).
 // Cross-wave hand-offs: the workgroup barriers carry workgroup-scope fences; every record written
 // inside the kernel is read back through vector loads (vgpr_index), never the scalar cache.
-template <int F>
-__global__ void __launch_bounds__(WinoCfg<F>::NWV * 64)
+// threads of the persistent kernel's workgroup: the Winograd f32 tower's, or the bf16 tower's
+template <int F, bool BF16> struct SimsCfg { static constexpr int NT = WinoCfg<F>::NWV * 64; };
+template <int F> struct SimsCfg<F, true> {
+    static_assert(TowerCfg<F>::BPB == 1, "persistent bf16 kernel: one board per workgroup");
+    static constexpr int NT = (F / (16 * TowerCfg<F>::NCO)) * TowerCfg<F>::WB * 64;
+};
+template <int F, bool BF16>
+__global__ void __launch_bounds__((SimsCfg<F, BF16>::NT))
 k_sims32w(Engine E, TowerArgs ta, SearchOut so, int step0, int step1) {
     __shared__ int s_kind;
     if (!E.active[vgpr_index(blockIdx.x)]) return;     // constant within a move
@@ -1639,7 +1657,10 @@ k_sims32w(Engine E, TowerArgs ta, SearchOut so, int step0, int step1) {
         t1 = __builtin_amdgcn_s_memtime();
         c_tree += t1 - t0;
 #endif
-        if (kind == X_ROW) tower32w_board<F, true>(nullptr, ta, g, nullptr, nullptr, so, tid);
+        if (kind == X_ROW) {
+            if constexpr (BF16) tower_board<F, true>(nullptr, ta, g, 1, nullptr, nullptr, so, tid);
+            else tower32w_board<F, true>(nullptr, ta, g, nullptr, nullptr, so, tid);
+        }
         __syncthreads();
 #ifdef AZ_SIMS_TRACE
         t0 = __builtin_amdgcn_s_memtime();
@@ -1683,17 +1704,23 @@ static TowerArgs tower_args(const NetDev* n) {
     return ta;
 }
 
-bool sims_persistent_supported(const NetDev* n) { return tower_supported(n) && wino_supported(n); }
+bool sims_persistent_supported(const NetDev* n) {
+    return tower_supported(n) && (wino_supported(n) || (n->dtype == AZ_DTYPE_BF16 && n->filters == 64));
+}
 
 // simulation steps [step0, step1) of every game through k_sims32w (one workgroup per game);
 // ends with every simulation backed up
 int sims_persistent(const NetDev* n, const Engine& E, const SearchOut& so, int step0, int step1, hipStream_t st) {
     if (step1 <= step0) return 0;
-    if (!sims_persistent_supported(n)) return fail("persistent simulation kernel: needs the f32 Winograd tower");
+    if (!sims_persistent_supported(n)) return fail("persistent simulation kernel: needs the f32 Winograd tower or the bf16 64-filter tower");
     const TowerArgs ta = tower_args(n);
+    if (n->dtype == AZ_DTYPE_BF16) {
+        k_sims32w<64, true><<<E.G, SimsCfg<64, true>::NT, 0, st>>>(E, ta, so, step0, step1);
+        return hipGetLastError() == hipSuccess ? 0 : fail("persistent simulation kernel launch failed");
+    }
 #define AZ_SIMS32W(FF)                                                                                  \
     if (n->filters == FF) {                                                                            \
-        k_sims32w<FF><<<E.G, WinoCfg<FF>::NWV * 64, 0, st>>>(E, ta, so, step0, step1);                 \
+        k_sims32w<FF, false><<<E.G, SimsCfg<FF, false>::NT, 0, st>>>(E, ta, so, step0, step1);          \
         return hipGetLastError() == hipSuccess ? 0 : fail("persistent simulation kernel launch failed"); \
     }
     AZ_SIMS32W(256) AZ_SIMS32W(128) AZ_SIMS32W(64)

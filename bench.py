@@ -468,7 +468,7 @@ def main():
         "sim_step_ms": {k: tm[k + "_ms"] / max(tm["sim_steps"], 1)
                         for k in ("select", "expand", "encode", "tower", "heads", "backup")},
         "sim_kernels": ("k_sims32w<%d> for the untimed simulation steps: one workgroup per game runs its backup, "
-                        "select, expand and Winograd f32 evaluation with no grid-wide step boundary (the timed "
+                        "select, expand and network evaluation with no grid-wide step boundary (the timed "
                         "every-32nd steps, which carry the roofline / tree_walk events, run as separate kernels)"
                         % args.filters) if tm.get("persistent") else
                        "k_step (backup + select + expand) + the fused tower, two launches per simulation step",

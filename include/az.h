@@ -181,7 +181,8 @@ typedef struct {
 int az_search_stats_get(az_search* s, az_search_stats* out);
 /* 1 if the untimed simulation steps run through the persistent per-game kernel (k_sims32w: a
  * game's backup / select / expand and its Winograd f32 evaluation in one workgroup, no grid-wide
- * step boundary; chosen when the games fit the device in one round, the net is f32 Winograd and
+ * step boundary; chosen when the games fit the device in one round, the net is f32 Winograd (or the
+ * bf16 64-filter tower) and
  * the FEN cache is off; env AZ_PERSIST=0/1 forces it), 0 if they run as k_step + the batched
  * tower.  Either way the results are identical (tests/test_gpu_search.py). */
 int az_search_persistent(az_search* s);

@@ -196,20 +196,23 @@ def test_fused_step_kernel_matches_separate_kernels(require_gpu, monkeypatch, ca
     assert runs[0] == runs[1] == runs[2]
 
 
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
 @pytest.mark.parametrize("timing", [False, True])
-def test_persistent_sims_match_step_kernels(require_gpu, monkeypatch, timing):
+def test_persistent_sims_match_step_kernels(require_gpu, monkeypatch, timing, dtype):
     """k_sims32w (each game's simulation loop in one workgroup: backup, select, expand and the
-    Winograd f32 evaluation, no grid-wide step boundary) against k_step + the batched tower, and
+    evaluation -- Winograd f32 or the bf16 tower -- with no grid-wide step boundary) against
+    k_step + the batched tower, and
     against the timed mix (every 32nd simulation step through the separate kernels): identical
     visit counts, improved policies and depths of one search, identical simulation / evaluation /
     terminal-leaf counts over several self-play moves."""
-    net = A.AlphaZero(6, 64, weights=A.random_weights(6, 64, seed=42), dtype="f32")
+    net = A.AlphaZero(6, 64, weights=A.random_weights(6, 64, seed=42), dtype=dtype)
     runs = []
     for persist in ("1", "0"):
         monkeypatch.setenv("AZ_PERSIST", persist)
         s = A.BatchedSearch(net, games=24, sims=300, seed=29, cache_capacity=0)
         s.timing(reset=True, enable=timing)
         s.set_roots([[]] * 12 + [[588]] * 12, apply_noise=True)
+        assert s.persistent == (persist == "1")
         imp, vis, dep = s.run()
         st = s.stats()
         sp = A.SelfPlay(net, games=24, sims=72, seed=31, cache_capacity=0)
