@@ -1124,9 +1124,19 @@ template <> struct WinoCfg<256> {
     static constexpr int NWV = AZ_WINO_NWV, NN = 16 / NWV, XH = 1, XS = 1, CH = 32, PF = WINO_PF;
 };
 template <> struct WinoCfg<128> { static constexpr int NWV = 8, NN = 1, XH = 1, XS = 2, CH = 32, PF = WINO_PF; };
+#ifndef AZ_WINO64_PQ
+#define AZ_WINO64_PQ 0     // 1: point quarters (conv_wino_pq: 4 waves x 4 points x all 64 channels, wave-private transforms)
+#endif
+#ifndef AZ_WINO_PQ_SGB
+#define AZ_WINO_PQ_SGB 1   // 1: the point-quarter transform interleaved into the MFMAs by sched_group_barrier
+#endif
+#if AZ_WINO64_PQ
+template <> struct WinoCfg<64> { static constexpr int XH = 4, NWV = 4, NN = 4, XS = 1, CH = 64, PF = 4; };
+#else
 template <> struct WinoCfg<64> {
     static constexpr int XH = AZ_WINO64_XH, NWV = 4 * XH, NN = 1, XS = 2, CH = AZ_WINO64_CH, PF = AZ_WINO64_PF;
 };
+#endif
 // Winograd weight fragment offsets: wave w's lane base (output fragments NN cw.., its point half) and
 // the byte offset of ring step t (16-channel group kl = t / NXI, point t % NXI of the half) of chunk cg
 template <int F> __device__ __forceinline__ int wino_voff(int w, int lane) {
@@ -1483,6 +1493,185 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase, in
 #undef WT_STAMP
 }
 
+// Point quarters (F = 64, one board, 4 waves = one per SIMD): wave w owns the Winograd points
+// xi = 4w..4w+3 (row w of the 4x4 point grid) for all F output channels.  Row w of B^T d B needs
+// two patch rows, so each wave transforms only its own points into a wave-private V region: its
+// transform and its MFMAs need no workgroup barrier, and the transform of 16-channel group kc+1
+// runs under the MFMAs of group kc.  A^T M A needs all 16 points of a (channel, tile): every wave
+// passes its M rows through its V region (one barrier) and wave n finishes output fragment n with
+// the one-point-set kernel's arithmetic in the same order, so M and the outputs are bit-identical
+// to WinoCfg<64>{XH = 1} (the transforms compute the same rows, the MFMAs accumulate each point
+// over kc and s4 in the same order).  LDS: V region w = [kc 4][point 4][quad 4][tile slot 16][4]
+// f32 = 16 KB, reused for the M exchange ([fragment 4][point 4][64 lanes][4]).
+// wr: the weight ring, [PF steps][1][4 fragments]; step s = (kc = s / 4, point 4w + s % 4).
+template <int F, bool RESID>
+__device__ __forceinline__ void conv_wino_pq(char* __restrict__ ldsb, int vbase, const __amdgpu_buffer_rsrc_t rW,
+                                             const __amdgpu_buffer_rsrc_t rN, const float* __restrict__ bias,
+                                             f32x4 (&wr)[WinoCfg<F>::PF][1][WinoCfg<F>::NN],
+                                             f32x4 (&xres)[WinoCfg<F>::NN][4], int w, int lane) {
+    constexpr int CF = F / 16, RS = F / 4 + 2, R16 = RS * 16;
+    constexpr int NN = WinoCfg<F>::NN, PF = WinoCfg<F>::PF, NKC = F / 16, NST = NKC * 4;
+    static_assert(NN == CF && WinoCfg<F>::NWV == 4 && WinoCfg<F>::XS == 1 && NST % PF == 0, "point quarters");
+    const int l16 = lane & 15, h = lane >> 4;
+    const int ty = l16 >> 2, tx = l16 & 3;
+    const int vw = vbase + w * (NKC * 4096);                   // this wave's V region
+    // transform items: channel lane & 15 of the group, tile (it, lane >> 4), it = 0..3
+    const int tch = lane & 15, ttx = vgpr_index(lane >> 4);
+    // this wave's row of B^T: t = d[ra] + d[rb] (w = 1) or d[ra] - d[rb]
+    const int ra = w == 0 ? 0 : w == 2 ? 2 : 1, rb = w == 0 ? 2 : w == 1 ? 2 : w == 2 ? 1 : 3;
+    const bool tadd = w == 1;
+    // columns of the patch; off-board ones read the clamped columns 3 / 4 (distinct banks within
+    // each 32-lane group, as in conv_wino) and are zeroed
+    const int cs0 = ttx > 0 ? 2 * ttx - 1 : 3, cs3 = ttx < 3 ? 2 * ttx + 2 : 4;
+    const int ccol[4] = {cs0 * R16, 2 * ttx * R16, (2 * ttx + 1) * R16, cs3 * R16};
+    auto tload = [&](int kc, float (&d)[4][2][4]) {
+        const int chan = (kc * 16 + tch) * 4;
+#pragma unroll
+        for (int it = 0; it < 4; it++) {
+            // patch rows 2 it - 1 + ra / rb, clamped onto the board (zeroed in tstore)
+            const int pa = min(max(2 * it - 1 + ra, 0), 7), pb = min(max(2 * it - 1 + rb, 0), 7);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                d[it][0][j] = *reinterpret_cast<const float*>(ldsb + pa * 8 * R16 + ccol[j] + chan);
+                d[it][1][j] = *reinterpret_cast<const float*>(ldsb + pb * 8 * R16 + ccol[j] + chan);
+            }
+        }
+    };
+    auto tstore = [&](int kc, const float (&d)[4][2][4]) {
+        const int quad = tch >> 2;
+        char* vb = ldsb + vw + kc * 4096 + quad * 256 + (tch & 3) * 4;
+#pragma unroll
+        for (int it = 0; it < 4; it++) {
+            const bool oka = (unsigned)(2 * it - 1 + ra) < 8u, okb = (unsigned)(2 * it - 1 + rb) < 8u;
+            float t[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const bool okc = j == 0 ? ttx > 0 : j == 3 ? ttx < 3 : true;
+                const float ea = oka && okc ? d[it][0][j] : 0.f, eb = okb && okc ? d[it][1][j] : 0.f;
+                t[j] = tadd ? ea + eb : ea - eb;
+            }
+            const float v[4] = {t[0] - t[2], t[1] + t[2], t[2] - t[1], t[1] - t[3]};
+            const int slot = ((4 * it + ttx) ^ (AZ_WINO_SWZ * (quad & 3))) * 16;
+#pragma unroll
+            for (int c = 0; c < 4; c++) *reinterpret_cast<float*>(vb + c * 1024 + slot) = v[c];
+        }
+    };
+    // B fragment of step s: group s / 4, point 4w + s % 4 (the conv_wino V layout, one point set)
+    const int vrd = vw + h * 256 + ((l16 ^ (AZ_WINO_SWZ * h)) * 16);
+    auto bread = [&](int s) { return *reinterpret_cast<const f32x4*>(ldsb + vrd + (s >> 2) * 4096 + (s & 3) * 1024); };
+    const int co0 = w * 16 + h * 4;                              // the fragment this wave finishes
+    auto out_addr = [&](int a, int b) { return ((2 * ty + a) * 8 + 2 * tx + b) * R16 + co0 * 4; };
+    if constexpr (!RESID) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) xres[0][q] = *reinterpret_cast<const f32x4*>(ldsb + out_addr(q >> 1, q & 1));
+    }
+    f32x4 acc[4][NN];
+#pragma unroll
+    for (int x = 0; x < 4; x++)
+#pragma unroll
+        for (int n = 0; n < NN; n++) acc[x][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int voff = lane * 16 + 4 * w * CF * 1024;
+    float dn[4][2][4];
+    tload(0, dn);
+    tstore(0, dn);
+    // the V region is this wave's own: program order (LDS executes a wave's operations in order)
+    // is the only hand-off, the fence keeps the compiler from moving the reads above the writes
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    f32x4 Bc = bread(0);
+#pragma unroll
+    for (int s = 0; s < NST; s++) {
+        const int kc = s >> 2, j = s & 3;
+        const bool more = kc + 1 < NKC;
+        f32x4 Bn = Bc;
+        if (s + 1 < NST) Bn = bread(s + 1);
+        f32x4 a[NN];
+#pragma unroll
+        for (int n = 0; n < NN; n++) a[n] = wr[s % PF][0][n];
+        {   // refill with step s + PF (past this conv's end: the next conv's first steps)
+            const int tn = s + PF;
+            const bool nxt = tn >= NST;
+            const int t2 = nxt ? tn - NST : tn;
+            const int to = ((t2 >> 2) * 16 + (t2 & 3)) * CF * 1024;
+#pragma unroll
+            for (int n = 0; n < NN; n++)
+                wr[s % PF][0][n] = __builtin_bit_cast(
+                    f32x4, __builtin_amdgcn_raw_buffer_load_b128(nxt ? rN : rW, voff + n * 1024 + to, 0, 0));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; s4++)
+#pragma unroll
+            for (int n = 0; n < NN; n++) acc[j][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[n][s4], Bc[s4], acc[j][n], 0, 0, 0);
+        // one wave per SIMD: the next group's transform must issue between this step's MFMAs (a
+        // VALU or LDS instruction issues in the shadow of a 32-cycle MFMA), not after them
+        if (j == 0 && more) tload(kc + 1, dn);
+        if (j == 1 && more) tstore(kc + 1, dn);
+#if AZ_WINO_PQ_SGB
+        if (j == 0 && more) {
+#pragma unroll
+            for (int i = 0; i < 4 * NN; i++) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // DS read
+                __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);   // VALU
+            }
+        }
+        if (j == 1 && more) {
+#pragma unroll
+            for (int i = 0; i < 4 * NN; i++) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);   // VALU
+                __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);   // DS write
+            }
+        }
+#endif
+        __builtin_amdgcn_sched_barrier(0);
+        if (j == 1 && more) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        Bc = Bn;
+    }
+    // M exchange: [fragment n][point j][lane] in this wave's V region (its own reads are done:
+    // in order), then wave n gathers fragment n's 16 points from the 4 regions
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+    for (int n = 0; n < NN; n++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) *reinterpret_cast<f32x4*>(ldsb + vw + (n * 4 + j) * 1024 + lane * 16) = acc[j][n];
+    __syncthreads();
+    f32x4 m16[16];
+#pragma unroll
+    for (int x = 0; x < 16; x++)
+        m16[x] = *reinterpret_cast<const f32x4*>(ldsb + vbase + (x >> 2) * (NKC * 4096) + (w * 4 + (x & 3)) * 1024 + lane * 16);
+    {
+        const float4 bb = *reinterpret_cast<const float4*>(bias + co0);
+        f32x4 y[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            float m[4][4];
+#pragma unroll
+            for (int x = 0; x < 16; x++) m[x >> 2][x & 3] = m16[x][r];
+            float s0[4], s1[4];
+#pragma unroll
+            for (int jj = 0; jj < 4; jj++) {
+                s0[jj] = m[0][jj] + m[1][jj] + m[2][jj];
+                s1[jj] = m[1][jj] - m[2][jj] - m[3][jj];
+            }
+            const float br = r == 0 ? bb.x : r == 1 ? bb.y : r == 2 ? bb.z : bb.w;
+            y[0][r] = (s0[0] + s0[1] + s0[2]) + br;
+            y[1][r] = (s0[1] - s0[2] - s0[3]) + br;
+            y[2][r] = (s1[0] + s1[1] + s1[2]) + br;
+            y[3][r] = (s1[1] - s1[2] - s1[3]) + br;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            f32x4 v = y[q];
+            if constexpr (RESID) v += xres[0][q];
+#pragma unroll
+            for (int r = 0; r < 4; r++) v[r] = fmaxf(v[r], 0.0f);
+            *reinterpret_cast<f32x4*>(ldsb + out_addr(q >> 1, q & 1)) = v;
+        }
+    }
+    __syncthreads();
+}
+
 // one board (batch row row0) through the Winograd f32 tower, all NWV waves of the workgroup
 template <int F, bool SEARCH>
 __device__ __forceinline__ void tower32w_board(const float* __restrict__ planes, const TowerArgs& ta, int row0,
@@ -1532,7 +1721,17 @@ __device__ __forceinline__ void tower32w_board(const float* __restrict__ planes,
             conv32_lds<32, RSI, F, RSF, 1, NN, false>(ldsb, reinterpret_cast<char*>(X), vbase, zero_off, r0, rz, ta.b[0],
                                                       wr, w, 0, lane);
         };
-        if constexpr (XH == 1) {
+        if constexpr (XH == 4) {   // point quarters: every wave, one 16-channel fragment each
+            f32x4 wr[T32_PF][1];
+            const __amdgpu_buffer_rsrc_t r0 = t32_rsrc(ta.w[0], ta.wbytes[0]);
+            const __amdgpu_buffer_rsrc_t rz = t32_rsrc(ta.w[0] + 18 * (F / 16) * 64, ta.wbytes[0] - 18 * (F / 16) * 1024);
+            const int voff = (w * 64 + lane) * 16;
+#pragma unroll
+            for (int i = 0; i < T32_PF; i++)
+                wr[i][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r0, voff + i * (F / 16) * 1024, 0, 0));
+            conv32_lds<32, RSI, F, RSF, 1, 1, false>(ldsb, reinterpret_cast<char*>(X), vbase, zero_off, r0, rz, ta.b[0],
+                                                     wr, w, 0, lane);
+        } else if constexpr (XH == 1) {
             input_conv();
         } else {   // point halves: only the first NCW waves; the others meet its closing barrier
             if (w < NCW) input_conv();
@@ -1571,8 +1770,13 @@ __device__ __forceinline__ void tower32w_board(const float* __restrict__ planes,
 #endif
         const __amdgpu_buffer_rsrc_t r1 = t32_rsrc(ta.ww[2 * b], wb1), r2 = t32_rsrc(ta.ww[2 * b + 1], wb2);
         const __amdgpu_buffer_rsrc_t r3 = t32_rsrc(b + 1 < ta.blocks ? ta.ww[2 * b + 2] : ta.ww[2 * b + 1], wb3);
-        conv_wino<F, false>(ldsb, vbase, zero_off, r1, r2, ta.b[1 + 2 * b], wring, xres, w, lane, trw);
-        conv_wino<F, true>(ldsb, vbase, zero_off, r2, r3, ta.b[2 + 2 * b], wring, xres, w, lane);
+        if constexpr (XH == 4) {
+            conv_wino_pq<F, false>(ldsb, vbase, r1, r2, ta.b[1 + 2 * b], wring, xres, w, lane);
+            conv_wino_pq<F, true>(ldsb, vbase, r2, r3, ta.b[2 + 2 * b], wring, xres, w, lane);
+        } else {
+            conv_wino<F, false>(ldsb, vbase, zero_off, r1, r2, ta.b[1 + 2 * b], wring, xres, w, lane, trw);
+            conv_wino<F, true>(ldsb, vbase, zero_off, r2, r3, ta.b[2 + 2 * b], wring, xres, w, lane);
+        }
         if (b < 12) WC_STAMP(3 + b);
     }
 #ifdef AZ_WINO_TRACE
@@ -1705,6 +1909,11 @@ static TowerArgs tower_args(const NetDev* n) {
 }
 
 bool sims_persistent_supported(const NetDev* n) {
+#if defined(AZ_TOWER_TRACE) || defined(AZ_WINO_TRACE)
+    // trace builds stamp one tower launch into a buffer only tower_forward allocates (the
+    // persistent kernel's TowerArgs carry no trace buffer: its stamps would write through null)
+    return false;
+#endif
     return tower_supported(n) && (wino_supported(n) || (n->dtype == AZ_DTYPE_BF16 && n->filters == 64));
 }
 
