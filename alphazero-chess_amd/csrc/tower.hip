@@ -1072,7 +1072,7 @@ tower32_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __rest
 #define AZ_WINO_TLOAD 0    // step of a chunk at which the next chunk's patch reads issue
 #endif
 #ifndef AZ_WINO_TSPLIT
-#define AZ_WINO_TSPLIT 8   // steps between the patch reads and their transform + V writes
+#define AZ_WINO_TSPLIT 2   // steps between the patch reads and their transform + V writes (8 -> 2: C3 tower -1.8 to -2.6 %, profiles/r02_ab_wino_s9_knobs_c3.log)
 #endif
 #ifndef AZ_WINO_TSTAG
 #define AZ_WINO_TSTAG 16   // steps by which the second wave of each SIMD pair (w >= NWV / 2) delays its transform
