@@ -33,7 +33,7 @@ PEAK_F32_TFLOPS = 157.3       # MI355X_MICROARCH.md: f32 MFMA = vector peak
 PEAK_HBM_GBS = 8000.0         # MI355X_MICROARCH.md: 8.0 TB/s spec
 # HBM bytes per tower launch from rocprofv3 PMC passes (tools/pmc_run.sh: FETCH_SIZE x2 per the
 # gfx950 correction + WRITE_SIZE), same kernel and per-launch work (2048 rows, 20x256)
-PMC_SUMMARY = {"f32": os.path.join(ROOT, "profiles", "r02_pmc_tower32w_summary.json"),
+PMC_SUMMARY = {"f32": os.path.join(ROOT, "profiles", "r02_pmc_tower32w_s9_summary.json"),
                "bf16": os.path.join(ROOT, "profiles", "r01_pmc_tower_v11_summary.json")}
 # mean plies of complete self-play games of this config (tools/game_length.py: 256 games, 20x256
 # random-init seed 42, 800 sims/move, noise + temperature moves, played to the end)
