@@ -33,7 +33,8 @@ PEAK_F32_TFLOPS = 157.3       # MI355X_MICROARCH.md: f32 MFMA = vector peak
 PEAK_HBM_GBS = 8000.0         # MI355X_MICROARCH.md: 8.0 TB/s spec
 # HBM bytes per tower launch from rocprofv3 PMC passes (tools/pmc_run.sh: FETCH_SIZE x2 per the
 # gfx950 correction + WRITE_SIZE), same kernel and per-launch work (2048 rows, 20x256)
-PMC_SUMMARY = {"f32": os.path.join(ROOT, "profiles", "r02_pmc_tower32w_s9_summary.json"),
+PMC_SUMMARY = {"f32": os.path.join(ROOT, "profiles", "r02_pmc_tower32w_s9_summary.json"),          # Winograd
+               "f32-direct": os.path.join(ROOT, "profiles", "r02_pmc_tower32_summary.json"),      # AZ_WINOGRAD=0
                "bf16": os.path.join(ROOT, "profiles", "r01_pmc_tower_v11_summary.json")}
 # mean plies of complete self-play games of this config (tools/game_length.py: 256 games, 20x256
 # random-init seed 42, 800 sims/move, noise + temperature moves, played to the end)
@@ -44,10 +45,10 @@ TOLERANCE = {"f32": "value |d| <= 1e-5, policy |d| <= 1e-4 p + 1e-8 (tests/test_
                      "(tests/test_gpu_net.py)"}
 
 
-def pmc_traffic(games, blocks, filters, dtype):
+def pmc_traffic(games, blocks, filters, dtype, winograd=True):
     """Per-launch HBM traffic of the dominant kernel from the committed PMC summary, or None
     when the bench workload is not the one the counters were collected on."""
-    path = PMC_SUMMARY.get(dtype)
+    path = PMC_SUMMARY.get(dtype if dtype != "f32" or winograd else "f32-direct")
     if (games, blocks, filters) != (2048, 20, 256) or not path or not os.path.exists(path):
         return None, None
     with open(path) as f:
@@ -362,9 +363,9 @@ def main():
         FLOPs the kernel really issues over the same time (the kernel-efficiency figure)."""
         peak = PEAK_BF16_TFLOPS if dtype == "bf16" else PEAK_F32_TFLOPS
         conv_tflops = tm["conv_flop"] / (tm["conv_ms"] * 1e-3) / 1e12 if tm["conv_ms"] > 0 else 0.0
-        traffic, traffic_src = pmc_traffic(G, args.blocks, args.filters, dtype)
         kname = net.tower_kernel if net is not None else "none (rehearsal)"
         wino = net is not None and net.winograd
+        traffic, traffic_src = pmc_traffic(G, args.blocks, args.filters, dtype, wino or net is None)
         B, Fh = args.blocks, args.filters
         direct_row = 2.0 * 64.0 * (171.0 * Fh + 18.0 * B * Fh * Fh)
         exec_row = 2.0 * 64.0 * 171.0 * Fh + (2.0 * 64.0 * 18.0 * B * Fh * Fh / 2.25 if wino else 2.0 * 64.0 * 18.0 * B * Fh * Fh)
