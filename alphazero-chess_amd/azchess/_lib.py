@@ -15,7 +15,7 @@ ACTION_SPACE = 4096
 MAX_MOVES = 256
 ONGOING, DRAW, WHITE_WINS, BLACK_WINS, ILLEGAL = 0, 1, 2, 3, -1
 DTYPE_F32, DTYPE_BF16 = 0, 1
-EVAL_NET, EVAL_SYNTHETIC = 0, 1
+EVAL_NET, EVAL_SYNTHETIC, EVAL_CALLBACK = 0, 1, 2
 
 
 class AzPos(C.Structure):
@@ -57,6 +57,9 @@ class AzTiming(C.Structure):
                 ("rows", C.c_int64)]
 
 
+# az_eval_fn (include/az.h): int (*)(void* ctx, const az_pos*, int n, float* policy, float* value)
+EVAL_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(AzPos), C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_float))
+
 # every symbol include/az.h declares: (name, restype, argtypes)
 P = C.POINTER
 SIGNATURES = [
@@ -90,9 +93,11 @@ SIGNATURES = [
     ("az_search_default_cfg", C.c_int, [P(AzSearchCfg)]),
     ("az_search_create", C.c_int, [C.c_void_p, P(AzSearchCfg), C.c_int, P(C.c_void_p)]),
     ("az_search_destroy", C.c_int, [C.c_void_p]),
+    ("az_search_set_evaluator", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     ("az_search_set_roots", C.c_int, [C.c_void_p, P(C.c_int32), P(C.c_int32), P(C.c_int32), P(C.c_int32),
                                       C.c_int]),
     ("az_search_run", C.c_int, [C.c_void_p, P(C.c_float), P(C.c_uint32), P(C.c_int32)]),
+    ("az_search_read_roots", C.c_int, [C.c_void_p, P(C.c_float), P(C.c_uint32), P(C.c_int32)]),
     ("az_search_advance", C.c_int, [C.c_void_p, P(C.c_int32), C.c_int, P(C.c_int32)]),
     ("az_selfplay_reset", C.c_int, [C.c_void_p]),
     ("az_selfplay_step", C.c_int, [C.c_void_p, P(C.c_int), P(C.c_int)]),

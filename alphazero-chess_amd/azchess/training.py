@@ -239,7 +239,7 @@ def train(iterations, blocks=NUM_RES_BLOCKS, filters=NUM_FILTERS, games=NUM_EPIS
     for iteration in range(iterations):
         t0 = time.perf_counter()
         model = trainer.model(dtype)
-        new_unique, plays, sims_done, games_done = 0, 0, 0, 0
+        new_unique, plays, sims_done, games_done, steps_done, moves_done, finished = 0, 0, 0, 0, 0, 0, 0
         while True:
             sp = SelfPlay(model, games=games, sims=sims, device=device, continuous=False,
                           seed=seed + 1000003 * rank + 7919 * iteration + 104729 * plays)
@@ -248,10 +248,14 @@ def train(iterations, blocks=NUM_RES_BLOCKS, filters=NUM_FILTERS, games=NUM_EPIS
                 _, active = sp.step()
                 for st in sp.drain_raw():
                     new_unique += replay.add(st)
+                    steps_done += 1
                 if active == 0:
                     break
             plays += 1
-            sims_done += sp.search.stats()["sims"]
+            ss = sp.search.stats()
+            sims_done += ss["sims"]
+            moves_done += ss["moves"]
+            finished += ss["games_finished"]
             games_done += games
             if len(replay) >= min_replay:
                 break
@@ -266,7 +270,8 @@ def train(iterations, blocks=NUM_RES_BLOCKS, filters=NUM_FILTERS, games=NUM_EPIS
         t2 = time.perf_counter()
         st = {"iteration": iteration, "replay": len(replay), "new_unique": new_unique, "lr": lr,
               "policy_loss": pl_sum / max(train_steps, 1), "value_loss": vl_sum / max(train_steps, 1),
-              "selfplay_s": t1 - t0, "train_s": t2 - t1, "selfplay_games": games_done, "selfplay_sims": sims_done}
+              "selfplay_s": t1 - t0, "train_s": t2 - t1, "selfplay_games": games_done, "selfplay_sims": sims_done,
+              "games_finished": finished, "episode_steps": steps_done, "moves": moves_done}
         history.append(st)
         if log:
             log(st)

@@ -13,24 +13,50 @@ from .parameters import CACHE_CAPACITY, C_PUCT, DIRICHLET_ALPHA, DIRICHLET_EPSIL
 
 def make_cfg(games, sims=NUM_SIMULATIONS, c_puct=C_PUCT, dir_alpha=DIRICHLET_ALPHA, dir_eps=DIRICHLET_EPSILON,
              temp_moves=TEMPERATURE_ANNEALING, noise=True, seed=SEED, synthetic=False, continuous=False,
-             record_evals=False, eval_log_cap=0, cache_capacity=CACHE_CAPACITY):
+             record_evals=False, eval_log_cap=0, cache_capacity=CACHE_CAPACITY, callback=False):
+    kind = L.EVAL_CALLBACK if callback else (L.EVAL_SYNTHETIC if synthetic else L.EVAL_NET)
     return L.AzSearchCfg(games, sims, c_puct, dir_alpha, dir_eps, temp_moves, 1 if noise else 0, seed,
-                         L.EVAL_SYNTHETIC if synthetic else L.EVAL_NET, 1 if continuous else 0,
-                         1 if record_evals else 0, eval_log_cap, cache_capacity)
+                         kind, 1 if continuous else 0, 1 if record_evals else 0, eval_log_cap, cache_capacity)
+
+
+def _eval_trampoline(evaluator):
+    """az_eval_fn around a Python process_batch-style callable (training.rs:380-422):
+    evaluator(positions) -> (policy [n, 4096], value [n]); its rows are copied into the engine's
+    staging buffers."""
+    from .chess import Position
+
+    def fn(_ctx, pos, n, pol, val):
+        try:
+            states = [Position(L.AzPos.from_buffer_copy(pos[i])) for i in range(n)]
+            p, v = evaluator(states)
+            np.ctypeslib.as_array(pol, shape=(n * 4096,))[:] = np.asarray(p, np.float32).reshape(n * 4096)
+            np.ctypeslib.as_array(val, shape=(n,))[:] = np.asarray(v, np.float32).reshape(n)
+            return 0
+        except Exception:                       # an exception must not unwind through the C frames
+            import traceback
+            traceback.print_exc()
+            return 1
+    return L.EVAL_FN(fn)
 
 
 class BatchedSearch:
     """G concurrent game trees on one device."""
 
-    def __init__(self, model=None, games=1, device=0, **cfg):
-        synthetic = model is None
-        self.cfg = make_cfg(games, synthetic=synthetic, **cfg)
+    def __init__(self, model=None, games=1, device=0, evaluator=None, **cfg):
+        """model: an AlphaZero (AZ_EVAL_NET); evaluator: a caller-owned process_batch-style callable
+        (AZ_EVAL_CALLBACK); neither: the synthetic evaluator the oracle shares."""
+        synthetic = model is None and evaluator is None
+        self.cfg = make_cfg(games, synthetic=synthetic, callback=evaluator is not None, **cfg)
         self.games = games
         self.model = model
         h = C.c_void_p()
         L.check(L.lib.az_search_create(model._h if model is not None else None, C.byref(self.cfg), device,
                                        C.byref(h)))
         self._h = h
+        self._eval_fn = None
+        if evaluator is not None:
+            self._eval_fn = _eval_trampoline(evaluator)     # kept alive as long as the engine
+            L.check(L.lib.az_search_set_evaluator(self._h, C.cast(self._eval_fn, C.c_void_p), None))
 
     def __del__(self):
         try:
@@ -56,6 +82,15 @@ class BatchedSearch:
         vis = np.zeros((self.games, 4096), np.uint32)
         dep = np.zeros(self.games, np.int32)
         L.check(L.lib.az_search_run(self._h, L.fptr(imp), L.u32ptr(vis), L.i32ptr(dep)))
+        return imp, vis, dep
+
+    def read_roots(self):
+        """(improved [G,4096], visits [G,4096], depth [G]) of the current roots, no simulations run
+        (the reference's public MCTree fields, tree.rs:25-34)."""
+        imp = np.zeros((self.games, 4096), np.float32)
+        vis = np.zeros((self.games, 4096), np.uint32)
+        dep = np.zeros(self.games, np.int32)
+        L.check(L.lib.az_search_read_roots(self._h, L.fptr(imp), L.u32ptr(vis), L.i32ptr(dep)))
         return imp, vis, dep
 
     def advance(self, actions, apply_noise=True):

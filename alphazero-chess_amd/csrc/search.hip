@@ -443,6 +443,52 @@ __global__ void __launch_bounds__(64) k_finish(Engine E, int mode, const int* ac
     if (E.noise) root_noise(E, g, ngid, 0, gam, kpos, sh);
 }
 
+// ------------------------------------------------------------------ caller-owned evaluator
+// AZ_EVAL_CALLBACK (the reference's InferenceRequest / process_batch, training.rs:28-31, 380-422):
+// the rows' leaf positions go to the host in batch-row order, the caller's policy rows come back
+// and are read at each new node's legal move indices (MCTree::new, tree.rs:84-104).
+__global__ void __launch_bounds__(64) k_gather_rows(Engine E, const int* __restrict__ count_ptr, azc::Pos* out) {
+    const int row = blockIdx.x * blockDim.x + threadIdx.x;
+    if (row >= load_fresh(count_ptr)) return;
+    out[row] = E.npos[(size_t)E.row_game[row] * E.NMAX + E.row_node[row]];
+}
+
+__global__ void __launch_bounds__(64) k_apply_rows(const int* __restrict__ count_ptr, SearchOut so,
+                                                   const float* __restrict__ policy, const float* __restrict__ value) {
+    const int row = vgpr_index(blockIdx.x), lane = threadIdx.x;
+    if (row >= load_fresh(count_ptr)) return;
+    const int game = so.row_game[row], node = so.row_node[row];
+    const Node nd = so.nodes[(size_t)game * so.NMAX + node];
+    Edge* e = so.edges + (size_t)game * so.EMAX + nd.edge_begin;
+    const float* pr = policy + (size_t)row * AZ_ACTION_SPACE;
+    __shared__ int slot[2];
+    if (lane == 0) {
+        slot[0] = -1;
+        if (so.log_cap > 0) {
+            const int r = atomicAdd(&so.ctr->log_count, 1);
+            const int po = atomicAdd(&so.ctr->log_prior_count, (int)nd.nedges);
+            slot[0] = (r < so.log_cap && po + nd.nedges <= so.log_prior_cap) ? r : -1;
+            slot[1] = po;
+        }
+    }
+    __syncthreads();
+    for (int i = lane; i < nd.nedges; i += 64) {
+        const int idx = e[i].idx & azc::IDX_MASK;
+        const float P = pr[idx];
+        e[i].P = P;
+        if (slot[0] >= 0) { so.log_idx[slot[1] + i] = idx; so.log_prior[slot[1] + i] = P; }
+    }
+    if (lane == 0) {
+        so.value[row] = value[row];
+        if (slot[0] >= 0) {
+            so.log_key[slot[0]] = azc::fen_key(so.npos[(size_t)game * so.NMAX + node]);
+            so.log_value[slot[0]] = value[row];
+            so.log_off[slot[0]] = slot[1];
+            so.log_n[slot[0]] = nd.nedges;
+        }
+    }
+}
+
 // visits / improved policy / depth readout (dense 4096 per game)
 __global__ void k_readout(Engine E, float* improved, uint32_t* visits, int* depth) {
     const int g = vgpr_index(blockIdx.x);
@@ -498,6 +544,11 @@ struct az_search {
     int cus = 256;                   // compute units of the device
     std::vector<hipEvent_t> ev;      // 7 per sim step
     az_timing acc{};
+    // AZ_EVAL_CALLBACK: the caller's evaluator and its staging buffers (pinned host, device)
+    az_eval_fn eval_fn = nullptr;
+    void* eval_ctx = nullptr;
+    azc::Pos* h_pos = nullptr; float* h_pol = nullptr; float* h_val = nullptr;
+    azc::Pos* d_pos = nullptr; float* d_pol = nullptr; float* d_val = nullptr;
 };
 
 namespace {
@@ -522,6 +573,29 @@ unsigned long long sum_games(az_search* s, const unsigned long long* d) {
     unsigned long long t = 0;
     for (unsigned long long v : h) t += v;
     return t;
+}
+
+// AZ_EVAL_CALLBACK: the rows counted at *cnt (device) through the caller's evaluator -- one
+// host round trip per simulation step, like the reference's batcher (training.rs:369-373)
+int eval_callback(az_search* s, const int* cnt) {
+    Engine& E = s->E;
+    if (!s->eval_fn) return fail("AZ_EVAL_CALLBACK: no evaluator installed (az_search_set_evaluator)");
+    int n = 0;
+    AZ_HIP(hipMemcpyAsync(&n, cnt, 4, hipMemcpyDeviceToHost, s->st));
+    AZ_HIP(hipStreamSynchronize(s->st));
+    if (n < 0 || n > E.G) return fail("AZ_EVAL_CALLBACK: bad row count");
+    if (n == 0) return 0;
+    k_gather_rows<<<(n + 63) / 64, 64, 0, s->st>>>(E, cnt, s->d_pos);
+    AZ_HIP(hipGetLastError());
+    AZ_HIP(hipMemcpyAsync(s->h_pos, s->d_pos, (size_t)n * sizeof(azc::Pos), hipMemcpyDeviceToHost, s->st));
+    AZ_HIP(hipStreamSynchronize(s->st));
+    const int rc = s->eval_fn(s->eval_ctx, reinterpret_cast<const az_pos*>(s->h_pos), n, s->h_pol, s->h_val);
+    if (rc != 0) return fail("AZ_EVAL_CALLBACK: the evaluator returned " + std::to_string(rc));
+    AZ_HIP(hipMemcpyAsync(s->d_pol, s->h_pol, (size_t)n * AZ_ACTION_SPACE * 4, hipMemcpyHostToDevice, s->st));
+    AZ_HIP(hipMemcpyAsync(s->d_val, s->h_val, (size_t)n * 4, hipMemcpyHostToDevice, s->st));
+    k_apply_rows<<<n, 64, 0, s->st>>>(cnt, s->so, s->d_pol, s->d_val);
+    AZ_HIP(hipGetLastError());
+    return 0;
 }
 
 // network evaluation of step `step`'s rows (+ FEN cache insert); events 3, 7, 8, 4 when timed
@@ -554,7 +628,7 @@ int eval_step(az_search* s, int step, hipEvent_t* ev) {
     } else {
         if (ev) { (void)hipEventRecord(ev[3], st); (void)hipEventRecord(ev[7], st); (void)hipEventRecord(ev[8], st); }
         if (ev) (void)hipEventRecord(ev[4], st);
-        rc = synth_eval_rows(cnt, G, s->so, st);
+        rc = s->cfg.evaluator == AZ_EVAL_CALLBACK ? eval_callback(s, cnt) : synth_eval_rows(cnt, G, s->so, st);
         if (rc) return rc;
     }
     if (E.cache_mask >= 0) k_cache_insert<<<(G + 63) / 64, 64, 0, st>>>(E, step);
@@ -601,6 +675,7 @@ int eval_rows(az_search* s) {
         if (!rc) rc = net_heads_search(n, s->x, cnt, E.G, s->so, s->st);
         return rc;
     }
+    if (s->cfg.evaluator == AZ_EVAL_CALLBACK) return eval_callback(s, cnt);
     return synth_eval_rows(cnt, E.G, s->so, s->st);
 }
 
@@ -755,6 +830,7 @@ int upload_histories(az_search* s, const int32_t* hist, const int32_t* off, cons
 
 int setup_roots(az_search* s, int apply_noise, bool save_template) {
     Engine& E = s->E;
+    s->sim_cursor = 0;                 // new roots abandon any self-play move in progress
     AZ_HIP(hipMemsetAsync(E.ctr->batch_count, 0, sizeof(E.ctr->batch_count), s->st));
     k_root_setup<<<(E.G + 63) / 64, 64, 0, s->st>>>(E);
     int rc = eval_rows(s);
@@ -832,6 +908,8 @@ int az_search_default_cfg(az_search_cfg* c) {
 int az_search_create(az_net* net, const az_search_cfg* cfg, int device, az_search** out) {
     if (!cfg || !out) return fail("null argument");
     if (cfg->games <= 0 || cfg->sims <= 0 || cfg->sims > 60000) return fail("bad games/sims");
+    if (cfg->evaluator != AZ_EVAL_NET && cfg->evaluator != AZ_EVAL_SYNTHETIC && cfg->evaluator != AZ_EVAL_CALLBACK)
+        return fail("bad evaluator (AZ_EVAL_NET / AZ_EVAL_SYNTHETIC / AZ_EVAL_CALLBACK)");
     if (cfg->evaluator == AZ_EVAL_NET && !net) return fail("AZ_EVAL_NET needs a network");
     AZ_HIP(hipSetDevice(device));
     az_search* s = new az_search();
@@ -905,6 +983,14 @@ int az_search_create(az_net* net, const az_search_cfg* cfg, int device, az_searc
         rc |= dalloc(s, &p, (size_t)G * 64 * n->filters * ab); s->h = p;
         if (rc) { az_search_destroy(s); return -1; }
     }
+    if (cfg->evaluator == AZ_EVAL_CALLBACK) {
+        rc |= dalloc(s, &s->d_pos, G); rc |= dalloc(s, &s->d_pol, (size_t)G * AZ_ACTION_SPACE); rc |= dalloc(s, &s->d_val, G);
+        if (!rc && (hipHostMalloc((void**)&s->h_pos, (size_t)G * sizeof(azc::Pos)) != hipSuccess ||
+                    hipHostMalloc((void**)&s->h_pol, (size_t)G * AZ_ACTION_SPACE * 4) != hipSuccess ||
+                    hipHostMalloc((void**)&s->h_val, (size_t)G * 4) != hipSuccess))
+            rc = fail("hipHostMalloc failed (evaluator staging)");
+        if (rc) { az_search_destroy(s); return -1; }
+    }
     SearchOut& so = s->so;
     so.nodes = E.nodes; so.edges = E.edges; so.NMAX = E.NMAX; so.EMAX = E.EMAX;
     so.row_game = E.row_game; so.row_node = E.row_node; so.value = E.value;
@@ -920,9 +1006,19 @@ int az_search_destroy(az_search* s) {
     (void)hipSetDevice(s->device);
     if (s->st) (void)hipStreamSynchronize(s->st);
     for (void* p : s->allocs) (void)hipFree(p);
+    for (void* p : {(void*)s->h_pos, (void*)s->h_pol, (void*)s->h_val})
+        if (p) (void)hipHostFree(p);
     for (hipEvent_t e : s->ev) (void)hipEventDestroy(e);
     if (s->st) (void)hipStreamDestroy(s->st);
     delete s;
+    return 0;
+}
+
+int az_search_set_evaluator(az_search* s, az_eval_fn fn, void* ctx) {
+    if (!s || !fn) return fail("null argument");
+    if (s->cfg.evaluator != AZ_EVAL_CALLBACK) return fail("az_search_set_evaluator: cfg.evaluator is not AZ_EVAL_CALLBACK");
+    s->eval_fn = fn;
+    s->eval_ctx = ctx;
     return 0;
 }
 
@@ -937,13 +1033,7 @@ int az_search_set_roots(az_search* s, const int32_t* hist, const int32_t* off, c
     return rc;
 }
 
-int az_search_run(az_search* s, float* improved, uint32_t* visits, int32_t* depth) {
-    if (!s) return fail("null search");
-    if (!s->roots_fresh) return fail("az_search_run: set roots (az_search_set_roots / az_search_advance) first");
-    s->roots_fresh = false;
-    AZ_HIP(hipSetDevice(s->device));
-    int rc = run_sims(s);
-    if (rc) return rc;
+static int read_roots(az_search* s, float* improved, uint32_t* visits, int32_t* depth) {
     const int G = s->E.G;
     float* di = nullptr; uint32_t* dv = nullptr; int* dd = nullptr;
     if (improved) AZ_HIP(hipMalloc(&di, (size_t)G * AZ_ACTION_SPACE * 4));
@@ -957,6 +1047,22 @@ int az_search_run(az_search* s, float* improved, uint32_t* visits, int32_t* dept
     AZ_HIP(hipStreamSynchronize(s->st));
     (void)hipFree(di); (void)hipFree(dv); (void)hipFree(dd);
     return 0;
+}
+
+int az_search_run(az_search* s, float* improved, uint32_t* visits, int32_t* depth) {
+    if (!s) return fail("null search");
+    if (!s->roots_fresh) return fail("az_search_run: set roots (az_search_set_roots / az_search_advance) first");
+    s->roots_fresh = false;
+    AZ_HIP(hipSetDevice(s->device));
+    int rc = run_sims(s);
+    if (rc) return rc;
+    return read_roots(s, improved, visits, depth);
+}
+
+int az_search_read_roots(az_search* s, float* improved, uint32_t* visits, int32_t* depth) {
+    if (!s) return fail("null search");
+    AZ_HIP(hipSetDevice(s->device));
+    return read_roots(s, improved, visits, depth);
 }
 
 int az_search_advance(az_search* s, const int32_t* actions, int apply_noise, int32_t* result) {
@@ -976,6 +1082,7 @@ int az_search_advance(az_search* s, const int32_t* actions, int apply_noise, int
     AZ_HIP(hipMemcpy(res.data(), dr, G * 4, hipMemcpyDeviceToHost));
     (void)hipFree(da); (void)hipFree(dr);
     s->roots_fresh = true;
+    s->sim_cursor = 0;                 // re-rooted: a self-play move in progress is abandoned
     if (result) memcpy(result, res.data(), G * 4);
     return 0;
 }

@@ -296,6 +296,8 @@ __device__ __forceinline__ int move_index_bf(int from, int to, int turn) {
 }
 
 constexpr int GEN_WAVES = 4;   // waves per workgroup that may run gen_legal_wave (k_step STEP_WPB <= 4)
+// NW: waves of the workgroup that run it (the LDS staging rows it reserves; k_sims32w: wave 0 only)
+template <int NW = GEN_WAVES>
 __device__ __forceinline__ int gen_legal_wave(const azc::Pos& p, Edge* __restrict__ out, int lane, bool* in_check,
                                            bool* legal_ep, unsigned long long* tr = nullptr) {
     using namespace azc;
@@ -415,8 +417,8 @@ __device__ __forceinline__ int gen_legal_wave(const azc::Pos& p, Edge* __restric
     // moves are staged in LDS as (from, to, flag) at their positions -- the serial per-lane loop
     // (up to 27 targets for a queen) is then a few instructions an iteration -- and written out as
     // edges by one lane per move (move index computed once per move, coalesced 16-byte stores)
-    __shared__ uint32_t s_mv[GEN_WAVES][MAX_EDGES];
-    uint32_t* mv = s_mv[(threadIdx.x >> 6) % GEN_WAVES];
+    __shared__ uint32_t s_mv[NW][MAX_EDGES];
+    uint32_t* mv = s_mv[(threadIdx.x >> 6) % NW];
     auto put = [&](int pos, int f, int to, int fl) { mv[pos] = (uint32_t)f | (uint32_t)to << 6 | (uint32_t)fl << 4; };
     if (ep_to) put(__popcll(ep_mask & ((1ull << lane) - 1ull)), lane, p.ep, 0);
     while (t) {                                        // this lane's main group, ascending to-squares
@@ -444,6 +446,7 @@ __device__ __forceinline__ int gen_legal_wave(const azc::Pos& p, Edge* __restric
     return total;
 }
 
+template <int NW = GEN_WAVES>
 __device__ __forceinline__ int expand_leaf_wave(const Engine& E, int g, int lane, int* nid_out, int step = -1) {
     // g is wave-uniform, and a provably uniform index would turn the per-game loads below into
     // scalar (s_load) reads; the leaf records were written by vector stores of another launch
@@ -473,7 +476,7 @@ __device__ __forceinline__ int expand_leaf_wave(const Engine& E, int g, int lane
     if (tr && lane == 0) tr[11] = __builtin_amdgcn_s_memtime();
 #endif
     bool chk = false, lep = false;
-    const int n = gen_legal_wave(c, edges + ebeg, lane, &chk, &lep, tr);
+    const int n = gen_legal_wave<NW>(c, edges + ebeg, lane, &chk, &lep, tr);
 #ifdef AZ_STEP_TRACE
     if (step == AZ_STEP_TRACE && lane == 0) E.trace[(size_t)g * 16 + 5] = __builtin_amdgcn_s_memtime();
 #endif

@@ -1672,11 +1672,252 @@ __device__ __forceinline__ void conv_wino_pq(char* __restrict__ ldsb, int vbase,
     __syncthreads();
 }
 
-// one board (batch row row0) through the Winograd f32 tower, all NWV waves of the workgroup
+// ====================================================================== F = 256: per-wave transforms
+// conv_wino_dt: the 256-filter Winograd conv with NO shared transform buffer and no barrier inside
+// the conv.  Each of the 8 waves (2 per SIMD) owns 32 output channels x all 16 points x all 16
+// tiles (128 accumulators) and computes the input transform V = B^T d B it needs ITSELF, in
+// registers, straight in the MFMA B layout: lane (h, tile) transforms channel 4t + h of its tile
+// for input quarter t (4 channels), from a 4x4 patch read out of the padded activation image.  The
+// 8-fold duplicated transform (32 VALU + 16 ds_read_b32 per quarter per wave, against 32 MFMAs)
+// runs in the MFMAs' issue shadows, software-pipelined one quarter ahead (two 16-register V slots),
+// so a wave's matrix stream never waits on another wave: the round-2 kernel's 8 chunk barriers per
+// conv (and the V writes between them) are gone, which is where its 17 % idle matrix pipe went
+// (DESIGN.md section 5.4).  Two barriers per conv remain: after the MFMAs (every wave has read the
+// layer input) and after the epilogue (the output is the next conv's input).
+// LDS (one board): a zero guard, then ACTP -- the layer input f32, rows padded with zero rows
+// above and below, 9 squares per row (the 9th is a zero column that is also the left neighbour of
+// the next row's first square) and 11 pad words, so every patch element is base + immediate with no
+// bounds logic; square stride 257 words and row stride 2324 (= 20 mod 32) make the 32 lanes of each
+// ds_read_b32 hit 32 distinct banks (8 ty + 2 tx + h) -- then RES, the block input (the residual of
+// conv 2 and, after the tower, the heads' input) in the round-2 layout [64 squares][66 slots].
+// Weights [quarter t 64][point quad q 4][co/16 16][lane 64][4 points] f32 (winograd_f32, net.hip):
+// one coalesced dwordx4 per lane = 4 points of one (co, ci); an 8-slot register ring (one quarter)
+// refilled right after each slot's 4 MFMAs, across conv boundaries.
+constexpr int DT_BETA = 257;                     // words per square (256 channels + 1)
+constexpr int DT_ALPHA = 2324;                   // words per padded row (9 squares + 11)
+constexpr int DT_GUARD = 260;                    // zero words before ACTP (>= DT_BETA: the (-1, -1) neighbour; RES 16-B aligned)
+constexpr int DT_ACT_WORDS = 10 * DT_ALPHA;
+constexpr int DT_ACT_BYTES = (DT_GUARD + DT_ACT_WORDS) * 4;   // guard + ACTP
+constexpr int DT_RES_BYTES = 64 * 66 * 16;                     // RES, the round-2 [64][66 slots] layout
+#ifndef AZ_DT_RING
+#define AZ_DT_RING 4       // weight-ring slots (f32x4 each) a wave keeps in flight (8 = one input quarter)
+#endif
+constexpr int DT_RING = AZ_DT_RING;
+static_assert(DT_RING == 4 || DT_RING == 8, "ring of half or one quarter");
+static_assert(DT_ACT_BYTES % 16 == 0, "RES must start 16-B aligned");
+
+template <bool RESID>
+__device__ __forceinline__ void conv_wino_dt(char* __restrict__ ldsb, const __amdgpu_buffer_rsrc_t rW,
+                                             const __amdgpu_buffer_rsrc_t rN, const float* __restrict__ bias,
+                                             f32x4 (&wr)[DT_RING / 2][2], int w, int lane) {
+    constexpr int NQ = 64;                                      // input quarters (4 channels each)
+    constexpr int QB = 4 * 16 * 1024;                           // weight bytes per quarter (all co)
+    const int l16 = lane & 15, h = lane >> 4;
+    const int ty = l16 >> 2, tx = l16 & 3;
+    // patch element (r, c) of tile (ty, tx) = square (2ty - 1 + r, 2tx - 1 + c) = padded row 2ty + r,
+    // column 2tx - 1 + c (column -1 = the zero column 8 of the row above)
+    const int pbase = (DT_GUARD + 2 * ty * DT_ALPHA + (2 * tx - 1) * DT_BETA + h) * 4;
+    const int voff = (2 * w * 64 + lane) * 16;
+    f32x4 acc[16][2];
+#pragma unroll
+    for (int x = 0; x < 16; x++)
+#pragma unroll
+        for (int n = 0; n < 2; n++) acc[x][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float V[2][16];
+    // channel 4t + h of the patch: 16 ds_read_b32 at immediate offsets from one lane base
+    auto pread = [&](int cbyte, float (&d)[16]) {
+        const char* p = ldsb + cbyte;
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+            for (int c = 0; c < 4; c++) d[r * 4 + c] = *reinterpret_cast<const float*>(p + (r * DT_ALPHA + c * DT_BETA) * 4);
+    };
+    // B^T d B in place, the round-2 kernel's operation order (rows first): bit-identical V
+    auto transform = [&](float (&d)[16]) {
+        float t[4][4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            t[0][j] = d[0 * 4 + j] - d[2 * 4 + j];
+            t[1][j] = d[1 * 4 + j] + d[2 * 4 + j];
+            t[2][j] = d[2 * 4 + j] - d[1 * 4 + j];
+            t[3][j] = d[1 * 4 + j] - d[3 * 4 + j];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            d[r * 4 + 0] = t[r][0] - t[r][2];
+            d[r * 4 + 1] = t[r][1] + t[r][2];
+            d[r * 4 + 2] = t[r][2] - t[r][1];
+            d[r * 4 + 3] = t[r][1] - t[r][3];
+        }
+    };
+    pread(pbase, V[0]);
+    transform(V[0]);
+#pragma unroll 1
+    for (int g = 0; g < NQ / 4; g++) {
+        const int gb = vgpr_index(pbase + g * 64);              // channels 16g + 4j + h
+        const bool last = g + 1 == NQ / 4;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int cur = j & 1, nxt = cur ^ 1;
+            const bool more = j < 3 || !last;
+            // next quarter's patch into the other slot (its V was consumed by the last quarter's MFMAs)
+            if (more) pread(j < 3 ? gb + (j + 1) * 16 : gb + 64, V[nxt]);
+            // refills: quarter t + 1 of this conv, or quarter 0 of the next one (rN)
+            const bool wrap = j == 3 && last;
+            const int soff = wrap ? 0 : (j < 3 ? g * 4 + j + 1 : g * 4 + 4) * QB;
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+#pragma unroll
+                for (int n = 0; n < 2; n++) {
+                    // ring slot k = 2q + n holds slot k of this quarter; refilled with slot k + RING of
+                    // the sequence (this quarter's later slots, then the next quarter's)
+                    const int k = 2 * q + n;
+                    const f32x4 a = wr[(k % DT_RING) / 2][(k % DT_RING) % 2];
+#pragma unroll
+                    for (int p = 0; p < 4; p++)
+                        acc[4 * q + p][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[p], V[cur][4 * q + p], acc[4 * q + p][n], 0, 0, 0);
+                    const int kn = k + DT_RING;                 // slot of the sequence to fetch
+                    const bool nq = kn >= 8;                    // ... in the next quarter
+                    const int qs = (kn & 7) / 2, ns = (kn & 7) % 2;
+                    const bool use_n = nq && wrap;
+                    const int so2 = nq ? soff : (g * 4 + j) * QB;
+                    wr[(k % DT_RING) / 2][(k % DT_RING) % 2] = __builtin_bit_cast(
+                        f32x4, __builtin_amdgcn_raw_buffer_load_b128(use_n ? rN : rW, voff + (qs * 16 + ns) * 1024, so2, 0));
+                }
+            if (more) transform(V[nxt]);
+            // interleave: per slot (4 MFMAs) one weight refill, the patch reads up front and the next
+            // quarter's transform VALU spread over the MFMAs
+#ifndef AZ_DT_SGB
+#define AZ_DT_SGB 1
+#endif
+#if AZ_DT_SGB
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);        // 4 MFMAs
+                __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);        // 1 VMEM read (weight refill)
+                __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);        // 4 VALU (transform)
+                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);        // 2 DS reads (next patch)
+            }
+#endif
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    __syncthreads();                                            // every wave has read the layer input
+    // output transform Y = A^T M A, + bias (+ residual from RES), ReLU -> ACTP (and RES after conv 2)
+    const int co0 = w * 32 + h * 4;
+#pragma unroll
+    for (int n = 0; n < 2; n++) {
+        const float4 bb = *reinterpret_cast<const float4*>(bias + co0 + n * 16);
+        f32x4 y[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            float m[4][4];
+#pragma unroll
+            for (int x = 0; x < 16; x++) m[x >> 2][x & 3] = acc[x][n][r];
+            float s0[4], s1[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                s0[j] = m[0][j] + m[1][j] + m[2][j];
+                s1[j] = m[1][j] - m[2][j] - m[3][j];
+            }
+            const float br = r == 0 ? bb.x : r == 1 ? bb.y : r == 2 ? bb.z : bb.w;
+            y[0][r] = (s0[0] + s0[1] + s0[2]) + br;
+            y[1][r] = (s0[1] - s0[2] - s0[3]) + br;
+            y[2][r] = (s1[0] + s1[1] + s1[2]) + br;
+            y[3][r] = (s1[1] - s1[2] - s1[3]) + br;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int a = q >> 1, b = q & 1;
+            const int co = co0 + n * 16;
+            char* rp = ldsb + DT_ACT_BYTES + (((2 * ty + a) * 8 + 2 * tx + b) * 66) * 16 + co * 4;
+            f32x4 v = y[q];
+            if constexpr (RESID) v += *reinterpret_cast<const f32x4*>(rp);
+#pragma unroll
+            for (int r = 0; r < 4; r++) v[r] = fmaxf(v[r], 0.0f);
+            if constexpr (RESID) *reinterpret_cast<f32x4*>(rp) = v;
+            float* ap = reinterpret_cast<float*>(ldsb + (DT_GUARD + (2 * ty + a + 1) * DT_ALPHA + (2 * tx + b) * DT_BETA + co) * 4);
+#pragma unroll
+            for (int r = 0; r < 4; r++) ap[r] = v[r];
+        }
+    }
+    __syncthreads();
+}
+
+// one board (batch row row0) through the 256-filter Winograd f32 tower with per-wave transforms
+template <bool SEARCH>
+__device__ __forceinline__ void tower32w_board_dt(const float* __restrict__ planes, const TowerArgs& ta, int row0,
+                                                  float* __restrict__ pol_out, float* __restrict__ val_out,
+                                                  const SearchOut& so, int tid) {
+    constexpr int F = 256, NT = 512, NN = 2;
+    constexpr int RSF = F / 4 + 2, RSI = 32 / 4 + 2;
+    constexpr int PLANES_BYTES = 64 * RSI * 16, ZN = 16 + F / 4;
+    static_assert(PLANES_BYTES + ZN * 16 <= DT_ACT_BYTES, "input planes + zero row must fit in ACTP");
+    static_assert(HeadsScratch<1, NT, heads_npart(NT, true)>::FLOATS * 4 <= DT_ACT_BYTES, "heads scratch must fit in ACTP");
+    __shared__ __attribute__((aligned(16))) uint4 lds[(DT_ACT_BYTES + DT_RES_BYTES) / 16];
+    const int lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    char* ldsb = reinterpret_cast<char*>(lds);
+    uint4* RES = lds + DT_ACT_BYTES / 16;
+    // input conv 19 (32) -> F, direct f32 (conv32_lds): planes staged at the start of the ACTP
+    // region, its zero row behind them, output into RES
+    stage_planes_f32<1, RSI, NT>(lds, planes, so, row0, 1, tid);
+    for (int c = tid; c < ZN; c += NT) lds[PLANES_BYTES / 16 + c] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    {
+        f32x4 wr[T32_PF][NN];
+        const __amdgpu_buffer_rsrc_t r0 = t32_rsrc(ta.w[0], ta.wbytes[0]);
+        const __amdgpu_buffer_rsrc_t rz = t32_rsrc(ta.w[0] + 18 * (F / 16) * 64, ta.wbytes[0] - 18 * (F / 16) * 1024);
+        const int voff = ((w * NN) * 64 + lane) * 16;
+#pragma unroll
+        for (int i = 0; i < T32_PF; i++)
+#pragma unroll
+            for (int n = 0; n < NN; n++)
+                wr[i][n] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r0, voff + n * 1024 + i * (F / 16) * 1024, 0, 0));
+        conv32_lds<32, RSI, F, RSF, 1, NN, false>(ldsb, reinterpret_cast<char*>(RES), 0, PLANES_BYTES, r0, rz, ta.b[0],
+                                                  wr, w, 0, lane);   // ends with a barrier
+    }
+    // ACTP <- RES: zero the guard, pad rows / column / words, then the 64 squares
+    for (int c = tid; c < DT_ACT_BYTES / 16; c += NT) lds[c] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    for (int c = tid; c < 64 * 64; c += NT) {
+        const int sq = c >> 6, q = c & 63;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(ldsb + DT_ACT_BYTES + (sq * RSF + q) * 16);
+        float* ap = reinterpret_cast<float*>(ldsb + (DT_GUARD + ((sq >> 3) + 1) * DT_ALPHA + (sq & 7) * DT_BETA + 4 * q) * 4);
+#pragma unroll
+        for (int r = 0; r < 4; r++) ap[r] = v[r];
+    }
+    __syncthreads();
+    f32x4 wring[DT_RING / 2][2];
+    if (ta.blocks > 0) {
+        const __amdgpu_buffer_rsrc_t r = t32_rsrc(ta.ww[0], ta.wwbytes[0]);
+        const int voff = (2 * w * 64 + lane) * 16;
+#pragma unroll
+        for (int q = 0; q < DT_RING / 2; q++)
+#pragma unroll
+            for (int n = 0; n < 2; n++)
+                wring[q][n] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff + (q * 16 + n) * 1024, 0, 0));
+    }
+    for (int b = 0; b < ta.blocks; b++) {
+        const unsigned wb3 = b + 1 < ta.blocks ? ta.wwbytes[2 * b + 2] : 0u;   // after the last conv: nothing (reads 0)
+        const __amdgpu_buffer_rsrc_t r1 = t32_rsrc(ta.ww[2 * b], ta.wwbytes[2 * b]);
+        const __amdgpu_buffer_rsrc_t r2 = t32_rsrc(ta.ww[2 * b + 1], ta.wwbytes[2 * b + 1]);
+        const __amdgpu_buffer_rsrc_t r3 = t32_rsrc(b + 1 < ta.blocks ? ta.ww[2 * b + 2] : ta.ww[2 * b + 1], wb3);
+        conv_wino_dt<false>(ldsb, r1, r2, ta.b[1 + 2 * b], wring, w, lane);
+        conv_wino_dt<true>(ldsb, r2, r3, ta.b[2 + 2 * b], wring, w, lane);
+    }
+    // heads from RES (the last block's output), scratch in the ACTP region
+    heads_group<F, RSF, 1, NT, SEARCH, true>(reinterpret_cast<const char*>(RES), reinterpret_cast<float*>(lds), 0, 1,
+                                             row0, tid, ta.head_frag32, ta.head, pol_out, val_out, so, nullptr);
+}
+
+// one board (batch row row0) through the Winograd f32 tower with transform chunks shared by all NWV
+// waves (F = 64, 128; and F = 256 when built with AZ_WINO_DT=0)
 template <int F, bool SEARCH>
-__device__ __forceinline__ void tower32w_board(const float* __restrict__ planes, const TowerArgs& ta, int row0,
-                                               float* __restrict__ pol_out, float* __restrict__ val_out,
-                                               const SearchOut& so, int tid) {
+__device__ __forceinline__ void tower32w_board_shared(const float* __restrict__ planes, const TowerArgs& ta, int row0,
+                                                      float* __restrict__ pol_out, float* __restrict__ val_out,
+                                                      const SearchOut& so, int tid) {
     constexpr int NWV = WinoCfg<F>::NWV, NT = NWV * 64, NN = WinoCfg<F>::NN, XS = WinoCfg<F>::XS;
     constexpr int XH = WinoCfg<F>::XH, NCW = NWV / XH;    // waves of the direct input conv
     constexpr int RSF = F / 4 + 2, RSI = 32 / 4 + 2;
@@ -1790,6 +2031,19 @@ __device__ __forceinline__ void tower32w_board(const float* __restrict__ planes,
 #undef WC_STAMP
 }
 
+// one board (batch row row0) through the Winograd f32 tower, dispatching on F
+template <int F, bool SEARCH>
+__device__ __forceinline__ void tower32w_board(const float* __restrict__ planes, const TowerArgs& ta, int row0,
+                                               float* __restrict__ pol_out, float* __restrict__ val_out,
+                                               const SearchOut& so, int tid) {
+    if constexpr (F == 256 && AZ_WINO_DT) {
+        tower32w_board_dt<SEARCH>(planes, ta, row0, pol_out, val_out, so, tid);
+        return;
+    } else {
+        tower32w_board_shared<F, SEARCH>(planes, ta, row0, pol_out, val_out, so, tid);
+    }
+}
+
 template <int F, bool SEARCH>
 __global__ void __launch_bounds__(WinoCfg<F>::NWV * 64)
 tower32w_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __restrict__ count_ptr, int rows,
@@ -1838,7 +2092,7 @@ k_sims32w(Engine E, TowerArgs ta, SearchOut so, int step0, int step1) {
             if (step < step1) {
                 select_game(E, g, lane);
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-                kind = expand_leaf_wave(E, g, lane, &nid, step);
+                kind = expand_leaf_wave<1>(E, g, lane, &nid, step);   // wave 0 only
                 if (lane == 0) {
                     if (kind == X_ROW) {
                         E.row_game[g] = g;

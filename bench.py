@@ -38,7 +38,9 @@ PMC_SUMMARY = {"f32": os.path.join(ROOT, "profiles", "r02_pmc_tower32w_s9_summar
                "bf16": os.path.join(ROOT, "profiles", "r01_pmc_tower_v11_summary.json")}
 # mean plies of complete self-play games of this config (tools/game_length.py: 256 games, 20x256
 # random-init seed 42, 800 sims/move, noise + temperature moves, played to the end)
-GAME_LENGTH = os.path.join(ROOT, "profiles", "r01_game_length_256.json")
+# (f32 Winograd net, the headline's; the round-1 file used the bf16 net and is only a fallback)
+GAME_LENGTH = [os.path.join(ROOT, "profiles", "r03_game_length_c3_f32.json"),
+               os.path.join(ROOT, "profiles", "r01_game_length_256.json")]
 # stated tolerances of the two tower precisions against the f32 oracle (tests/test_gpu_net.py)
 TOLERANCE = {"f32": "value |d| <= 1e-5, policy |d| <= 1e-4 p + 1e-8 (tests/test_gpu_net.py)",
              "bf16": "value |d| <= 2e-2, policy |d| <= 5e-2 p + 2e-5, total variation <= 2e-2 "
@@ -165,6 +167,23 @@ def net_flop_per_eval(B, F):
     return 2.0 * 64.0 * (171.0 * F + 18.0 * B * F * F + 40.0 * F + 2048.0) + 2.0 * (32768.0 + 64.0)
 
 
+def tower_algo_flop_per_row(B, F):
+    """algorithmic (direct-conv) FLOPs the engine books per evaluated row (az_timing.conv_flop):
+    input conv + 2B residual 3x3 convs, SURVEY 8a A6 without the heads"""
+    return 2.0 * 64.0 * (171.0 * F + 18.0 * B * F * F)
+
+
+def tower_exec_flop_per_row(B, F, dtype, wino):
+    """MFMA FLOPs the fused tower issues per row: the input conv with its 19 input planes padded to
+    32 channels, the residual convs (Winograd: 16 points x 16 tiles x F x F per conv; direct: 64
+    squares x 9 taps x F x F), the heads' 1x1 F->40 conv padded to 48 rows (bf16 mode: split into
+    hi + lo bf16 fragments, twice the MFMAs) and the 32->64 policy conv.  The value MLP runs on
+    VALU.  Cross-check: PMC SQ_INSTS_MFMA x 2048 FLOP (profiles/*pmc*summary.json)."""
+    res = (16.0 * 16.0 if (wino and dtype != "bf16") else 64.0 * 9.0) * 2.0 * F * F * 2 * B
+    heads = 2.0 * 64.0 * 48.0 * F * (2 if dtype == "bf16" else 1) + 2.0 * 64.0 * 64.0 * 32.0
+    return 2.0 * 64.0 * 9.0 * 32.0 * F + res + heads
+
+
 def config_name(games, sims, blocks, filters):
     """Which BASELINE.json config this run is: C3 = configs[2] (the headline), C2 = configs[1]."""
     if (sims, blocks, filters) == (800, 20, 256) and games == 2048:
@@ -182,6 +201,44 @@ def _free_port():
     return p
 
 
+def auto_sims_per_step(S, steps, warmup):
+    """Bench step size: the smallest divisor K >= 40 of S (or S) with steps*K and warmup*K whole
+    moves, so the timed window starts at a move boundary and carries its share of move completions
+    (k_finish, EpisodeStep drain, re-root); 100 if none (then window_move_aligned = false)."""
+    for K in range(min(40, S), S + 1):
+        if S % K == 0 and (steps * K) % S == 0 and (warmup * K) % S == 0:
+            return K
+    return 100 if S % 100 == 0 else S
+
+
+def play_games_leg(A, device, seed, world, barrier, synchronize, games=256, sims=800, blocks=6, filters=64):
+    """C2 (BASELINE.json configs[1]: 256 games x 800 sims/move, 6x64 f32 net) from startpos until
+    every game has ended (run_all_episodes, training.rs:340-378): completed games / wall time of
+    the slowest rank.  A measurement, not a projection; the C3 headline's games/hr is projected
+    (a C3 game at 800 sims takes tens of minutes)."""
+    from azchess.dist import reduce_run
+    net = A.AlphaZero(blocks, filters, dtype="f32", device=device, seed=42)
+    sp = A.SelfPlay(net, games=games, sims=sims, device=device, continuous=False, seed=seed + 7, cache_capacity=0)
+    sp.reset()
+    barrier()
+    t0 = time.perf_counter()
+    while True:
+        _, active = sp.step()
+        sp.drain_raw()                 # EpisodeSteps leave the engine as in the reference (memory.rs input)
+        if active == 0:
+            break
+    synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    st = sp.search.stats()
+    dt_max, tot = reduce_run(dt, [st["games_finished"], st["moves"], st["sims"]], world)
+    del sp, net
+    return {"value": tot[0] / dt_max * 3600.0, "unit": "games/hr", "games": int(tot[0]),
+            "plies_mean": tot[1] / max(tot[0], 1), "wall_s": dt_max, "sims_per_s": tot[2] / dt_max,
+            "config": "C2 (BASELINE.json configs[1]): %d games/GPU x %d sims/move, %dx%d f32 net, played from "
+                      "startpos to the end (not continuous: the batch shrinks as games end)" % (games, sims, blocks, filters)}
+
+
 def launch_ranks(n):
     """`bench.py --gpus N` without a torchrun environment: start N fresh child processes of this
     script, one per GPU (RANK = LOCAL_RANK = i, WORLD_SIZE = N, rendezvous on 127.0.0.1), and exit
@@ -192,9 +249,24 @@ def launch_ranks(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    rcs = [p.wait() for p in procs]
-    bad = [rc for rc in rcs if rc != 0]
-    return bad[0] if bad else 0
+    # poll: a rank that dies before the rendezvous must not leave its siblings blocked in
+    # init_process_group for gloo's default timeout -- terminate them and return its status
+    while True:
+        rcs = [p.poll() for p in procs]
+        bad = [rc for rc in rcs if rc not in (None, 0)]
+        if bad:
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+            return bad[0]
+        if all(rc == 0 for rc in rcs):
+            return 0
+        time.sleep(0.2)
 
 
 class _RehearsalSearch:
@@ -255,7 +327,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--games", type=int, default=2048)
     ap.add_argument("--sims", type=int, default=800)
-    ap.add_argument("--sims-per-step", type=int, default=100, help="simulation steps of every game per bench step")
+    ap.add_argument("--sims-per-step", type=int, default=0,
+                    help="simulation steps of every game per bench step (0 = auto: the smallest divisor of "
+                         "--sims >= 40 that makes the warmup and the timed window whole moves)")
     ap.add_argument("--blocks", type=int, default=20)
     ap.add_argument("--filters", type=int, default=256)
     ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"],
@@ -271,6 +345,12 @@ def main():
     ap.add_argument("--train-steps", type=int, default=5, help="timed training steps (0 = skip the training phase)")
     ap.add_argument("--train-batch", type=int, default=512, help="positions per rank (BATCH_SIZE, parameters.rs:17)")
     ap.add_argument("--train-timeout", type=int, default=240)
+    ap.add_argument("--games-leg", type=int, default=1,
+                    help="1: also play C2's games (256 x 800 sims, 6x64 f32) from startpos to the end on every rank "
+                         "and report the measured games/hr (0 = skip)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="test only: every rank runs on device 0 and the RCCL training leg is skipped (exercises the "
+                         "N>1 rank path with the real engine on a 1-GPU box; not a scaling measurement)")
     ap.add_argument("--rehearse", action="store_true",
                     help="no GPU: run the rank plumbing with a CPU stub engine (gloo); numbers are meaningless")
     ap.add_argument("--train-child", action="store_true", help=argparse.SUPPRESS)
@@ -291,8 +371,11 @@ def main():
     if world != args.gpus:
         raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     G, S, K = args.games, args.sims, args.sims_per_step
+    if K == 0:
+        K = auto_sims_per_step(S, args.steps, args.warmup)
     if K < 1 or S % K:
         raise SystemExit("bench.py: --sims-per-step must divide --sims")
+    aligned = (args.steps * K) % S == 0 and (args.warmup * K) % S == 0
 
     if args.rehearse:
         A = None
@@ -312,6 +395,9 @@ def main():
 
         def synchronize():
             A._lib.check(A._lib.lib.az_device_synchronize(local))
+    if args.same_device:
+        local = 0
+        ndev = max(ndev, world)
     if ndev < world or local >= ndev:
         raise SystemExit("bench.py: %d ranks need %d GPUs, %d visible" % (world, world, ndev))
     if world > 1:
@@ -352,36 +438,61 @@ def main():
         c = [st1[k] - st0[k] for k in ("sims", "evals", "terminal_leaves", "moves", "max_depth_sum", "cache_hits")]
         assert c[0] == G * K * steps, (c[0], G * K * steps)
         elapsed, tot = reduce_run(elapsed, c + [finished], world)
+        digests = None
+        if world > 1 and not args.rehearse:
+            # per-rank fingerprint of the games (the current roots' visit arrays): distinct seeds
+            # must give distinct games on every rank
+            import hashlib
+            _, vis, dep = sp.search.read_roots()
+            digests = [None] * world
+            dist.all_gather_object(digests, hashlib.sha1(vis.tobytes() + dep.tobytes()).hexdigest()[:16])
         del sp
-        return elapsed, dict(zip(("sims", "evals", "terminal", "moves", "depth", "hits", "finished"), tot)), tm, c[0]
+        res = dict(zip(("sims", "evals", "terminal", "moves", "depth", "hits", "finished"), tot))
+        res["rank_root_digests"] = digests
+        return elapsed, res, tm, c[0]
 
     def roofline(tm, dtype, net):
-        """The fused tower over the timed region.  achieved = ALGORITHMIC FLOPs (the direct 3x3
-        convs' 2*64*(171F + 18BF^2) per row, SURVEY 8a A6 without the heads) / tower time.  With the
-        Winograd tower the kernel executes 2.25x fewer multiplies on the 40 residual convs than that
-        algorithmic count, so `frac` can exceed 1; `executed_tflops` / `executed_frac` are the MFMA
-        FLOPs the kernel really issues over the same time (the kernel-efficiency figure)."""
+        """The fused tower over the timed region (HIP events around its launch on the engine stream,
+        every 32nd simulation step).  achieved / frac = the MFMA FLOPs the kernel EXECUTES per launch
+        (what the matrix pipe does: SURVEY 8d's roofline for the tower) / its measured time vs the
+        dense peak of that MFMA dtype; with the Winograd tower that is 1/2.25 of the direct-conv
+        multiplies on the residual convs.  algorithmic_tflops = the reference's direct-conv FLOPs
+        (SURVEY 8a A6, 2*64*(171F + 18BF^2) per row) over the same time: an equivalent rate, not a
+        fraction of any peak.  traffic = HBM bytes per launch from the committed PMC passes;
+        traffic_ratio = traffic / the algorithmic bytes (every weight once + the rows' I/O)."""
         peak = PEAK_BF16_TFLOPS if dtype == "bf16" else PEAK_F32_TFLOPS
-        conv_tflops = tm["conv_flop"] / (tm["conv_ms"] * 1e-3) / 1e12 if tm["conv_ms"] > 0 else 0.0
+        launches = max(tm["conv_launches"], 1)
+        rows = tm["conv_flop"] / max(tower_algo_flop_per_row(args.blocks, args.filters), 1.0)
+        secs = tm["conv_ms"] * 1e-3
         kname = net.tower_kernel if net is not None else "none (rehearsal)"
         wino = net is not None and net.winograd
-        traffic, traffic_src = pmc_traffic(G, args.blocks, args.filters, dtype, wino or net is None)
         B, Fh = args.blocks, args.filters
-        direct_row = 2.0 * 64.0 * (171.0 * Fh + 18.0 * B * Fh * Fh)
-        exec_row = 2.0 * 64.0 * 171.0 * Fh + (2.0 * 64.0 * 18.0 * B * Fh * Fh / 2.25 if wino else 2.0 * 64.0 * 18.0 * B * Fh * Fh)
-        exec_tflops = conv_tflops * exec_row / direct_row
-        return {"bound": "mfma", "achieved": conv_tflops, "peak": peak, "unit": "TFLOP/s",
-                "frac": conv_tflops / peak, "traffic": traffic,
+        exec_row = tower_exec_flop_per_row(B, Fh, dtype, wino or net is None)
+        exec_tflops = exec_row * rows / secs / 1e12 if secs > 0 else 0.0
+        algo_tflops = tm["conv_flop"] / secs / 1e12 if secs > 0 else 0.0
+        traffic, traffic_src = pmc_traffic(G, B, Fh, dtype, wino or net is None)
+        # algorithmic bytes per launch: every weight of the net once (transformed Winograd weights
+        # when the kernel uses them) + per row an 80-B packed position in and <= 218 priors out
+        wb = 4.0 * ((16.0 if wino else 9.0) * Fh * Fh * 2 * B + 9 * 32 * Fh + 48 * Fh + 64 * 32 + 512 * 64) \
+            if dtype != "bf16" else 2.0 * (9.0 * Fh * Fh * 2 * B + 9 * 32 * Fh) + 4.0 * (48 * Fh + 64 * 32 + 512 * 64)
+        algo_bytes = wb + (rows / launches) * (80.0 + 218 * 4.0 + 4.0)
+        return {"bound": "mfma", "achieved": exec_tflops, "peak": peak, "unit": "TFLOP/s",
+                "frac": exec_tflops / peak, "traffic": traffic,
                 "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
-                "kernel": "%s: input conv + %d residual convs + heads in one launch, %s; algorithmic FLOPs = direct-conv "
-                          "FLOPs; %d launches timed (HIP events on every 32nd simulation step)"
+                "algorithmic_bytes_per_launch": algo_bytes,
+                "traffic_ratio": (traffic / algo_bytes) if traffic else None,
+                "kernel": "%s: input conv + %d residual convs + heads in one launch, %s; %d launches timed (HIP events "
+                          "on every 32nd simulation step)"
                           % (kname, 2 * B, "v_mfma_f32_16x16x32_bf16" if dtype == "bf16" else "v_mfma_f32_16x16x4_f32",
                              tm["conv_launches"]),
-                "executed_tflops": exec_tflops, "executed_frac": exec_tflops / peak,
-                "executed_note": ("Winograd F(2x2,3x3): the residual convs execute 1/2.25 of the algorithmic multiplies"
-                                  if wino else "direct convolution: executed = algorithmic"),
-                "flop_per_launch": tm["conv_flop"] / max(tm["conv_launches"], 1),
-                "avg_ms_per_launch": tm["conv_ms"] / max(tm["conv_launches"], 1)}
+                "executed_flop_per_row": exec_row,
+                "executed_note": ("Winograd F(2x2,3x3): the residual convs execute 1/2.25 of the direct-conv "
+                                  "multiplies; input conv (19 -> 32 padded channels) and the heads' MFMAs included"
+                                  if wino else "direct convolution, input channels padded 19 -> 32, heads included"),
+                "algorithmic_tflops": algo_tflops,
+                "algorithmic_note": "direct-conv FLOPs of SURVEY 8a A6 (no heads) / tower time: an equivalent rate",
+                "rows_per_launch": rows / launches,
+                "avg_ms_per_launch": tm["conv_ms"] / launches}
 
     def make_net(dtype):
         if args.rehearse:
@@ -420,8 +531,13 @@ def main():
                      "cache_hit_frac": t2["hits"] / max(t2["sims"], 1), "entries": args.cache}
         del netc
 
+    # measured games/hr: C2's configuration played to the end on every rank (training.rs:294-378)
+    games_leg = None
+    if args.games_leg and not args.rehearse:
+        games_leg = play_games_leg(A, local, sh["seed"], world, barrier, synchronize)
+
     training = None
-    if args.train_steps > 0 and not args.rehearse:
+    if args.train_steps > 0 and not args.rehearse and not args.same_device:
         training = train_phase(args, A, rank, world, local)
     if rank != 0:
         dist.destroy_process_group()
@@ -455,8 +571,11 @@ def main():
                    "games_per_gpu": G, "sims_per_move": S, "blocks": args.blocks, "filters": args.filters,
                    "sims_per_step": K,
                    "step": "%d simulation steps of every game (a move = %d steps)" % (K, S // K),
+                   "window_move_aligned": aligned,
                    "fen_cache": "off (measured: 1 % hit rate over a 20-move C3 window, -14 % at C2; DESIGN.md section 6)",
-                   "parallelism": "games sharded %d-way, no collective (gloo barrier/max only)" % world},
+                   "parallelism": ("games sharded %d-way, no collective (gloo barrier/max only)" % world) +
+                                  (" -- TEST MODE: every rank on device 0 (--same-device), not a scaling "
+                                   "measurement" if args.same_device else "")},
         "roofline": roof,
         "tower": {"achieved_tflops": tower_tflops, "frac": tower_tflops / peak,
                   "ms_per_sim_step": tm["tower_ms"] / max(tm["sim_steps"], 1)},
@@ -479,18 +598,21 @@ def main():
         "avg_search_depth": depth_all / max(moves_all, 1),
         "games_finished": int(fin_all),
         "games_per_hr": fin_all / elapsed * 3600.0,
+        "games_per_hr_measured": games_leg,
+        "rank_root_digests": tot["rank_root_digests"],
         "games_per_hr_projected": None,
         "cpu_baseline": None,
         "training": training,
     }
-    if (args.blocks, args.filters, S) == (20, 256, 800) and os.path.exists(GAME_LENGTH) and not args.rehearse:
-        with open(GAME_LENGTH) as f:
+    gl_path = next((p for p in GAME_LENGTH if os.path.exists(p)), None)
+    if (args.blocks, args.filters, S) == (20, 256, 800) and gl_path and not args.rehearse:
+        with open(gl_path) as f:
             gl = json.load(f)
         # continuous self-play keeps every slot busy (a finished game restarts in its slot), so
         # the steady state plays sims/s / (sims/move * plies/game) games
         out["games_per_hr_projected"] = {
             "value": value * 3600.0 / (S * gl["plies_mean"]), "plies_per_game": gl["plies_mean"],
-            "source": os.path.relpath(GAME_LENGTH, ROOT),
+            "source": os.path.relpath(gl_path, ROOT), "game_length_net": gl.get("net"),
             "note": "projection, not a measurement: measured sims/s / (800 sims x mean plies of %d complete games "
                     "of a separate run); the timed window (%d x %d simulation steps) is too short for games to "
                     "finish" % (gl["games"], args.steps, K)}

@@ -101,7 +101,18 @@ int az_net_forward_device(az_net* net, const float* d_planes, int n, float* d_po
                           void* stream);
 
 /* ---- search: tree.rs MCTree + training.rs self-play driver ------------------------ */
-enum { AZ_EVAL_NET = 0, AZ_EVAL_SYNTHETIC = 1 };
+/* AZ_EVAL_NET: the engine's own az_net (fused HIP tower).  AZ_EVAL_SYNTHETIC: the hash evaluator
+ * the oracle shares (parity tests).  AZ_EVAL_CALLBACK: a caller-owned evaluator installed with
+ * az_search_set_evaluator -- the reference's InferenceRequest / process_batch boundary
+ * (training.rs:28-31, 380-422; tree.rs:222-228), e.g. a Rust caller keeping its burn model. */
+enum { AZ_EVAL_NET = 0, AZ_EVAL_SYNTHETIC = 1, AZ_EVAL_CALLBACK = 2 };
+/* Caller-owned evaluator: called on the calling thread of az_search_set_roots / az_search_run /
+ * az_selfplay_* once per simulation step with the n leaf positions that need an evaluation (every
+ * game's pending InferenceRequest of that step, in batch-row order).  It fills policy[n * 4096]
+ * (AlphaZero::forward's softmax row, agent.rs:128-130: the engine reads it at the legal move
+ * indices only) and value[n] (side-to-move view, tanh output).  Return 0 on success; a non-zero
+ * return aborts the search call with an error.  Buffers are engine-owned and valid for the call. */
+typedef int (*az_eval_fn)(void* ctx, const az_pos* positions, int n, float* policy, float* value);
 typedef struct {
     int games;          /* concurrent games G on this GPU (NUM_EPISODES, parameters.rs:13) */
     int sims;           /* simulations per move (NUM_SIMULATIONS, parameters.rs:32) */
@@ -111,7 +122,7 @@ typedef struct {
     int temp_moves;     /* TEMPERATURE_ANNEALING, parameters.rs:31 */
     int noise;          /* Dirichlet noise at roots (training.rs:358, tree.rs:243) */
     uint64_t seed;      /* counter-based RNG seed (replaces thread_rng) */
-    int evaluator;      /* AZ_EVAL_NET or AZ_EVAL_SYNTHETIC */
+    int evaluator;      /* AZ_EVAL_NET, AZ_EVAL_SYNTHETIC or AZ_EVAL_CALLBACK */
     int continuous;     /* self-play: restart a finished slot with a new game */
     int record_evals;   /* keep a log of every evaluation (for replay parity) */
     int eval_log_cap;   /* log capacity in rows */
@@ -124,15 +135,23 @@ typedef struct az_search az_search;
 int az_search_default_cfg(az_search_cfg* cfg);   /* reference defaults (parameters.rs) */
 int az_search_create(az_net* net, const az_search_cfg* cfg, int device, az_search** out);
 int az_search_destroy(az_search* s);
+/* Install the AZ_EVAL_CALLBACK evaluator (cfg.evaluator must be AZ_EVAL_CALLBACK); replaces
+ * process_batch (training.rs:380-422).  Must precede the first az_search_set_roots /
+ * az_selfplay_reset. */
+int az_search_set_evaluator(az_search* s, az_eval_fn fn, void* ctx);
 
 /* Roots from histories: game g's root = startpos + hist[off[g]..off[g+1]) (move indices),
  * evaluated and optionally noised: MCTree::new(policy, state, apply_noise), tree.rs:84-104.
- * noise_ply[g] (may be NULL = 0) selects the RNG stream (seed, game_id[g], ply). */
+ * noise_ply[g] (may be NULL = 0) selects the RNG stream (seed, game_id[g], ply).  Abandons a
+ * self-play move left in progress by az_selfplay_run_sims (its simulations are discarded). */
 int az_search_set_roots(az_search* s, const int32_t* hist, const int32_t* off, const int32_t* game_id,
                         const int32_t* noise_ply, int apply_noise);
 /* monte_carlo_tree_search for every game (tree.rs:106-115 / 169-178).  Outputs (any may
  * be NULL): improved policy [G,4096], visits [G,4096], max_subtree_depth [G]. */
 int az_search_run(az_search* s, float* improved, uint32_t* visits, int32_t* depth);
+/* The current roots' visits / improved policy / max_subtree_depth without running simulations:
+ * the reference's public MCTree fields (tree.rs:25-34), e.g. mid-move during az_selfplay_run_sims. */
+int az_search_read_roots(az_search* s, float* improved, uint32_t* visits, int32_t* depth);
 /* traverse_new(action, apply_noise) for every game (tree.rs:239-256) after playing the
  * action on its GameState (training.rs:323-325).  result[g] receives the play_move result. */
 int az_search_advance(az_search* s, const int32_t* actions, int apply_noise, int32_t* result);

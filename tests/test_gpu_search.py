@@ -245,3 +245,131 @@ def test_selfplay_matches_committed_search_golden(require_gpu):
         assert np.float32(s.final_value) == g["synth_final_value"][i], i
         ref = {int(k): float(v) for k, v in zip(g["synth_vis_idx"][off[i]:off[i + 1]], g["synth_vis_n"][off[i]:off[i + 1]])}
         assert s.visits == ref, i
+
+
+M64 = (1 << 64) - 1
+
+
+def _splitmix64(x):
+    x = (x + 0x9E3779B97F4A7C15) & M64
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & M64
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & M64
+    return x ^ (x >> 31)
+
+
+def synthetic_process_batch(states, calls=None):
+    """A caller-owned evaluator (process_batch, training.rs:380-422, written outside the engine)
+    that restates the synthetic evaluator the oracle shares (net.hip synth_eval_kernel): priors
+    1 + splitmix64(key ^ (idx + 1) * phi) >> 48 over the distinct legal indices, normalised in f32;
+    value (splitmix64(key ^ c) % 2001 - 1000) / 1000.  Unlisted policy entries get garbage: the
+    engine must read the row at the legal indices only."""
+    n = len(states)
+    if calls is not None:
+        calls.append(n)
+    pol = np.full((n, 4096), 7.0, np.float32)
+    val = np.zeros(n, np.float32)
+    for r, p in enumerate(states):
+        key = p.fen_key()
+        idx = np.unique(p.legal_indices())
+        w = [1 + (_splitmix64(key ^ (((int(i) + 1) * 0x9E3779B97F4A7C15) & M64)) >> 48) for i in idx]
+        tot = np.float32(sum(w))
+        pol[r, idx] = np.array(w, np.float32) / tot
+        val[r] = np.float32(int(_splitmix64(key ^ 0x5BD1E9955BD1E995) % 2001) - 1000) / np.float32(1000.0)
+    return pol, val
+
+
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_callback_evaluator_reproduces_synthetic_bit_exact(require_gpu, monkeypatch, fused):
+    """AZ_EVAL_CALLBACK (az_search_set_evaluator, the reference's InferenceRequest / process_batch
+    boundary): a Python evaluator equal to the synthetic one gives bit-identical visits, improved
+    policies and depths -- through the search API and through whole self-play games -- with one
+    batched call per simulation step (plus the root evaluation)."""
+    monkeypatch.setenv("AZ_FUSED_STEPS", fused)
+    hs = histories(6, 41)
+    S = 24
+    calls = []
+    cb = A.BatchedSearch(None, games=len(hs), sims=S, noise=True, seed=17,
+                         evaluator=lambda st: synthetic_process_batch(st, calls))
+    ref = A.BatchedSearch(None, games=len(hs), sims=S, noise=True, seed=17)
+    for s in (cb, ref):
+        s.set_roots(hs, apply_noise=True)
+    a, b = cb.run(), ref.run()
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+    assert 2 <= len(calls) <= 1 + S and calls[0] == len(hs) and max(calls) <= len(hs)   # no call for an empty step
+    st_cb, st_ref = cb.stats(), ref.stats()
+    assert (st_cb["sims"], st_cb["evals"], st_cb["terminal_leaves"]) == \
+           (st_ref["sims"], st_ref["evals"], st_ref["terminal_leaves"])
+    assert sum(calls[1:]) == st_cb["evals"]
+    # whole games through the self-play driver (run_all_episodes with a caller evaluator)
+    _, steps_cb = A.run_all_episodes(None, games=3, sims=8, seed=5, evaluator=synthetic_process_batch)
+    _, steps_ref = A.run_all_episodes(None, games=3, sims=8, seed=5)
+    key = lambda s: (s.game_id, s.ply, s.action, s.search_depth, s.result, np.float32(s.final_value),
+                     tuple(sorted(s.visits.items())))
+    assert sorted(map(key, steps_cb)) == sorted(map(key, steps_ref))
+
+
+def test_callback_evaluator_errors_surface(require_gpu):
+    def bad(states):
+        raise RuntimeError("evaluator down")
+    s = A.BatchedSearch(None, games=2, sims=4, seed=1, evaluator=bad)
+    with pytest.raises(A._lib.AzError, match="evaluator returned"):
+        s.set_roots([[], [588]], apply_noise=False)
+
+
+def _play_moves(sp, moves, k):
+    """`moves` self-play moves: through sp.step() (k = None) or run_sims(k) chunks."""
+    done = 0
+    while done < moves:
+        if k is None:
+            sp.step()
+            done += 1
+        else:
+            _, active, move_done = sp.run_sims(k)
+            assert (active >= 0) == move_done
+            done += move_done
+    st = sp.search.stats()
+    return ((st["sims"], st["evals"], st["terminal_leaves"], st["moves"], st["overflow"]),
+            sorted((s.game_id, s.ply, s.action, s.search_depth, s.result, tuple(sorted(s.visits.items())))
+                   for s in sp.drain()))
+
+
+@pytest.mark.parametrize("evaluator", ["net", "synthetic"])
+def test_run_sims_chunks_match_whole_moves(require_gpu, monkeypatch, evaluator):
+    """az_selfplay_run_sims (the bench's unit: a move cut into K-simulation chunks) against
+    az_selfplay_step (whole moves): identical EpisodeSteps and sims / evals / terminal counts for
+    K in {1, 7, 100, S}, timing on and off, persistent kernel on and off (6x64 f32 Winograd net),
+    with chunk edges that fall on and off the every-32nd timed steps."""
+    S, G, moves = 100, 8, 3
+    net = A.AlphaZero(6, 64, weights=A.random_weights(6, 64, seed=42), dtype="f32") if evaluator == "net" else None
+    # continuous: the games that end restart in their slot, so every move has work in every slot
+    mk = lambda: A.SelfPlay(net, games=G, sims=S, seed=37, continuous=True, cache_capacity=0)
+    for persist in (("1", "0") if net is not None else ("0",)):
+        monkeypatch.setenv("AZ_PERSIST", persist)
+        for timing in (False, True):
+            sp = mk()
+            sp.reset()
+            sp.search.timing(reset=True, enable=timing)
+            want = _play_moves(sp, moves, None)
+            assert want[0][0] == G * S * moves and want[0][4] == 0
+            for k in (1, 7, 100, S):
+                sp = mk()
+                sp.reset()
+                sp.search.timing(reset=True, enable=timing)
+                assert _play_moves(sp, moves, k) == want, (persist, timing, k)
+
+
+def test_set_roots_abandons_a_move_in_progress(require_gpu):
+    """a chunked move left half done must not leak its simulation cursor into the
+    search API on the same handle (new roots start a fresh move)."""
+    s = A.BatchedSearch(None, games=2, sims=16, seed=3, continuous=True)
+    sp = A.SelfPlay.__new__(A.SelfPlay)
+    sp.search, sp.games = s, 2
+    sp.reset()
+    assert sp.run_sims(5)[2] is False
+    s.set_roots([[], [588]], apply_noise=False)
+    imp, vis, dep = s.run()
+    assert np.all(vis.sum(1) == 16)
+    sp.reset()
+    fin, act = sp.step()          # a whole move again: the cursor is at 0
+    assert act == 2

@@ -153,3 +153,42 @@ def test_full_loop_selfplay_replay_train(require_gpu):
     assert hist[1]["lr"] == A.get_cyclical_lr(1)
     step_ms, ar_ms, n = tr.timing()
     assert n == 6 and step_ms > 0 and ar_ms < 1.0
+
+
+def test_c5_full_loop_20x256(require_gpu):
+    """C5 (BASELINE.json configs[4]) at its network size on one GPU: one iteration of train()
+    (training.rs:71-200) with the 20x256 f32 net -- 256 self-play games played to the end on the
+    Winograd tower, memory.rs replay, 2 AdamW steps on 512-position batches -- at 8 sims/move so
+    that it fits a test.  Checks: every game ends and every searched move becomes an EpisodeStep;
+    the replay holds >= 512 positions; losses finite; one more AdamW step at 20x256 bit-exact
+    against the float32 restatement (T.adamw_step, fresh moments); the trained net's forward within
+    the f32 tolerance of the oracle on 4 replay positions."""
+    import oracle as O
+    B, F, G = 20, 256, 256
+    tr, replay, hist = A.train(1, blocks=B, filters=F, games=G, sims=8, min_replay=512, train_steps=2,
+                               batch_size=512, dtype="f32")
+    h = hist[0]
+    assert h["games_finished"] == h["selfplay_games"] == G
+    assert h["episode_steps"] == h["moves"] > G
+    assert len(replay) >= 512
+    assert np.isfinite(h["policy_loss"]) and np.isfinite(h["value_loss"])
+    # one AdamW step at 20x256 from the trained weights, bit-exact
+    planes, pol, val, _ = replay.sample_arrays(512, seed=99)
+    t2 = A.Trainer(B, F, weights=tr.params(), max_batch=512)
+    t2.compute_gradients(planes, pol, val)
+    g = t2.grads()
+    p = t2.params()
+    lr = A.get_cyclical_lr(1)
+    t2.apply(lr)
+    mask = T.trainable_mask(B, F)
+    want, _, _ = T.adamw_step(p, g, np.zeros_like(p), np.zeros_like(p), mask, 1, lr)
+    got = t2.params()
+    assert np.array_equal(got, want), np.abs(got - want).max()
+    # the trained network on the inference engine (model.valid(), training.rs:83) vs the oracle
+    net = tr.model(dtype="f32")
+    assert net.winograd                  # the headline's f32 Winograd tower
+    x = planes[:4].reshape(4, 19, 8, 8)
+    gp, gv = net.forward(x)
+    rp, rv = O.RefNet(B, F, tr.params()).forward(x)
+    assert np.all(np.abs(gv - rv) <= 1e-5), np.abs(gv - rv).max()
+    assert np.all(np.abs(gp - rp) <= 1e-4 * rp + 1e-8)
