@@ -14,9 +14,6 @@ static_assert(sizeof(azc::Pos) == sizeof(az_pos), "Pos == az_pos");
 #ifndef AZ_WINOGRAD_DEFAULT
 #define AZ_WINOGRAD_DEFAULT 1
 #endif
-#ifndef AZ_WINO_DT
-#define AZ_WINO_DT 1       // F = 256 Winograd tower with per-wave transforms (tower.hip conv_wino_dt) and its weight layout
-#endif
 
 namespace azi {
 

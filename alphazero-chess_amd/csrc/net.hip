@@ -433,14 +433,10 @@ std::vector<float> swizzle_f32(const std::vector<float>& wf, int cout, int cin_r
 // Winograd F(2x2,3x3) weights U = G g G^T (f64, rounded once), fragment-swizzled for the MFMA A
 // operand: [ci/16][xi][co/16][lane][4], lane = co%16 + 16*((ci%16)/4), component ci%4, then 8 zero
 // steps (ring refills past the end); tap = dy*3 + dx as in swizzle_f32
-// F = 256 with AZ_WINO_DT (conv_wino_dt): [quarter t = ci/4][point quad q][co/16][lane][4 points xi = 4q + p],
-// lane = co%16 + 16*(ci%4): one dwordx4 per lane holds 4 points of one (co, ci); no pad (past the last
-// quarter the ring reads the next conv, or a zero-record descriptor)
 std::vector<float> winograd_f32(const std::vector<float>& wf, int F) {
     static const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
     const int CF = F / 16, NSTEP = (F / 16) * 16;
-    const bool dt = F == 256 && AZ_WINO_DT;
-    std::vector<float> o(dt ? (size_t)16 * F * F : (size_t)(NSTEP + 8) * CF * 64 * 4, 0.0f);
+    std::vector<float> o((size_t)(NSTEP + 8) * CF * 64 * 4, 0.0f);
     for (int co = 0; co < F; co++)
         for (int ci = 0; ci < F; ci++) {
             const float* g = &wf[((size_t)co * F + ci) * 9];
@@ -450,11 +446,6 @@ std::vector<float> winograd_f32(const std::vector<float>& wf, int F) {
             for (int a = 0; a < 4; a++)
                 for (int b = 0; b < 4; b++) {
                     const double u = gg[a][0] * G[b][0] + gg[a][1] * G[b][1] + gg[a][2] * G[b][2];
-                    if (dt) {
-                        const int xi = a * 4 + b, lane = (co % 16) + 16 * (ci % 4);
-                        o[((((size_t)(ci / 4) * 4 + xi / 4) * CF + co / 16) * 64 + lane) * 4 + xi % 4] = (float)u;
-                        continue;
-                    }
                     const int step = (ci / 16) * 16 + a * 4 + b;
                     const int lane = (co % 16) + 16 * ((ci % 16) / 4);
                     o[(((size_t)step * CF + co / 16) * 64 + lane) * 4 + ci % 4] = (float)u;

@@ -733,17 +733,6 @@ int run_sims(az_search* s, int i0 = 0, int i1 = -1) {
     }
     if (pending >= 0) k_backup<<<(s->E.G * 64 + 255) / 256, 256, 0, s->st>>>(s->E, pending);
     AZ_HIP(hipGetLastError());
-#ifdef AZ_SIMS_TRACE   // experiment: k_sims32w phase totals per game so far (tools/sims_trace.py)
-    if (pers && i1 >= s->E.S) {
-        std::vector<unsigned long long> h((size_t)s->E.G * 16);
-        AZ_HIP(hipStreamSynchronize(s->st));
-        AZ_HIP(hipMemcpy(h.data(), s->E.trace, h.size() * 8, hipMemcpyDeviceToHost));
-        if (FILE* f = fopen(getenv("AZ_SIMS_TRACE_FILE") ? getenv("AZ_SIMS_TRACE_FILE") : "sims_trace.bin", "ab")) {
-            fwrite(h.data(), 8, h.size(), f);
-            fclose(f);
-        }
-    }
-#endif
 #ifdef AZ_STEP_TRACE
     if (i0 <= AZ_STEP_TRACE && AZ_STEP_TRACE < i1) {
         std::vector<unsigned long long> h((size_t)s->E.G * 16);
@@ -948,7 +937,7 @@ int az_search_create(az_net* net, const az_search_cfg* cfg, int device, az_searc
     rc |= dalloc(s, &E.batch_hist, S);
     rc |= dalloc(s, &E.cached_value, G);
     rc |= dalloc(s, &E.g_sims, G); rc |= dalloc(s, &E.g_sel_bytes, G);
-#if defined(AZ_STEP_TRACE) || defined(AZ_SIMS_TRACE)
+#ifdef AZ_STEP_TRACE
     rc |= dalloc(s, &E.trace, (size_t)G * 16);
 #endif
     E.cache_mask = -1;

@@ -577,8 +577,11 @@ def main():
                                   (" -- TEST MODE: every rank on device 0 (--same-device), not a scaling "
                                    "measurement" if args.same_device else "")},
         "roofline": roof,
-        "tower": {"achieved_tflops": tower_tflops, "frac": tower_tflops / peak,
-                  "ms_per_sim_step": tm["tower_ms"] / max(tm["sim_steps"], 1)},
+        "tower": {"algorithmic_tflops": tower_tflops,
+                  "note": "the whole network's direct-conv FLOPs (SURVEY 8a A6, heads included) / tower time: an "
+                          "equivalent rate, not a fraction of a peak (roofline.frac is the executed-MFMA fraction)",
+                  "ms_per_sim_step": tm["tower_ms"] / max(tm["sim_steps"], 1),
+                  "share_of_step": (tm["tower_ms"] / max(tm["sim_steps"], 1)) * K / (elapsed / args.steps * 1e3)},
         "tolerance_vs_f32_oracle": TOLERANCE[args.dtype],
         "bf16_mode": bf16_res,
         "tree_walk": {"kernel": "k_select", "achieved_gbs": sel_gbs, "peak_gbs": PEAK_HBM_GBS,

@@ -1,7 +1,7 @@
 """Complete self-play games with the bench's net and search (20x256 random-init seed 42, 800
 sims/move, Dirichlet noise, temperature moves, training.rs:294-378) until every game ends:
 game-length distribution and the directly measured games/hr at this batch size.
-Usage: python tools/game_length.py [games] [out.json]"""
+Usage: python tools/game_length.py [games] [out.json] [f32|bf16]   (f32 = the headline's Winograd tower)"""
 import json
 import os
 import sys
@@ -15,7 +15,8 @@ import azchess as A  # noqa: E402
 
 G = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 out = sys.argv[2] if len(sys.argv) > 2 else None
-net = A.AlphaZero(20, 256, dtype="bf16", seed=42)
+dtype = sys.argv[3] if len(sys.argv) > 3 else "f32"
+net = A.AlphaZero(20, 256, dtype=dtype, seed=42)
 sp = A.SelfPlay(net, games=G, sims=800, continuous=False, seed=42, cache_capacity=0)
 sp.reset()
 t0 = time.perf_counter()
@@ -35,7 +36,8 @@ while True:
 dt = time.perf_counter() - t0
 L = np.array(list(plies.values()))
 st = sp.search.stats()
-res = {"games": G, "sims_per_move": 800, "net": "20x256 bf16 random-init seed 42", "wall_s": dt,
+res = {"games": G, "sims_per_move": 800, "net": "20x256 %s random-init seed 42 (%s)" % (dtype, net.tower_kernel),
+       "wall_s": dt,
        "games_per_hr_measured": G / dt * 3600, "sims_per_s": st["sims"] / dt,
        "plies_mean": float(L.mean()), "plies_median": float(np.median(L)), "plies_min": int(L.min()),
        "plies_max": int(L.max()),

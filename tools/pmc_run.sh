@@ -17,5 +17,6 @@ run() { name=$1; shift; timeout -s KILL 90 rocprofv3 --pmc "$@" --kernel-trace -
 run fetch FETCH_SIZE
 run write WRITE_SIZE
 run sq SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_WAVES
+run tcc TCC_HIT_sum TCC_MISS_sum
 run cyc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES
 rm -f $OUT/w.f32

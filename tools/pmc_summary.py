@@ -15,7 +15,7 @@ pat = sys.argv[2] if len(sys.argv) > 2 else "tower_kernel"
 mfma_cyc = float(sys.argv[3]) if len(sys.argv) > 3 else 16.0
 res = {"kernel_pattern": pat}
 durs = []
-for sub in ("fetch", "write", "sq", "cyc"):
+for sub in ("fetch", "write", "sq", "tcc", "cyc"):
     f = os.path.join(d, sub, sub + "_counter_collection.csv")
     if not os.path.exists(f):
         continue
@@ -37,6 +37,8 @@ if "FETCH_SIZE" in res and "WRITE_SIZE" in res:
     res["hbm_read_bytes_corrected"] = res["FETCH_SIZE"] * 1024 * 2
     res["hbm_write_bytes"] = res["WRITE_SIZE"] * 1024
     res["traffic_bytes"] = res["hbm_read_bytes_corrected"] + res["hbm_write_bytes"]
+if "TCC_HIT_sum" in res and "TCC_MISS_sum" in res:
+    res["l2_hit_rate"] = res["TCC_HIT_sum"] / max(res["TCC_HIT_sum"] + res["TCC_MISS_sum"], 1)
 if "SQ_LDS_IDX_ACTIVE" in res:
     res["lds_conflict_frac"] = res["SQ_LDS_BANK_CONFLICT"] / max(res["SQ_LDS_IDX_ACTIVE"], 1)
 if "SQ_WAVE_CYCLES" in res:
