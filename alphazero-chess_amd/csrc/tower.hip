@@ -975,16 +975,23 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase,
         tstore(0, d0);
     }
     __syncthreads();
+    // B fragment of this wave's step t: 16-channel group t / 16 of the chunk, point t % 16
+    auto boff = [](int t) { return (t / 16) * 1024 + (t % 16) * XST; };
+#ifdef AZ_WINO_NOBAR   // timing experiment only (wrong results): no chunk barrier, B read-ahead across chunks
+    f32x4 bq[LA];
+#pragma unroll
+    for (int i = 0; i < LA; i++) bq[i] = *reinterpret_cast<const f32x4*>(ldsb + vbase + vrd + boff(i));
+#endif
 #pragma unroll 1
     for (int c = 0; c < NCHUNK; c++) {
         float dn[IT][4][4];
         const int vb = vbase + (c & 1) * VBYTES + vrd;
-        // B fragment of this wave's step t: 16-channel group t / 16 of the chunk, point t % 16
-        auto boff = [](int t) { return (t / 16) * 1024 + (t % 16) * XST; };
         const bool more = c + 1 < NCHUNK;
+#ifndef AZ_WINO_NOBAR
         f32x4 bq[LA];
 #pragma unroll
         for (int i = 0; i < LA; i++) bq[i] = *reinterpret_cast<const f32x4*>(ldsb + vb + boff(i));
+#endif
 #pragma unroll
         for (int st = 0; st < SPX; st++) {
             f32x4 B[XS];
@@ -993,6 +1000,9 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase,
                 const int t = st * XS + xs;
                 B[xs] = bq[t % LA];
                 if (t + LA < SPC) bq[t % LA] = *reinterpret_cast<const f32x4*>(ldsb + vb + boff(t + LA));
+#ifdef AZ_WINO_NOBAR
+                else if (more) bq[t % LA] = *reinterpret_cast<const f32x4*>(ldsb + vbase + ((c + 1) & 1) * VBYTES + vrd + boff(t + LA - SPC));
+#endif
             }
             f32x4 a[XS][NN];
 #pragma unroll
@@ -1040,8 +1050,13 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase,
                 if (st == (TSG + WINO_TSPLIT) / XS && more && late) tstore((c + 1) & 1, dn);
             }
         }
+#ifndef AZ_WINO_NOBAR
         __syncthreads();
+#endif
     }
+#ifdef AZ_WINO_NOBAR
+    __syncthreads();
+#endif
     // output transform Y = A^T M A per (output fragment n, channel r), + bias (+ residual), ReLU
 #pragma unroll
     for (int n = 0; n < NN; n++) {
@@ -1131,9 +1146,17 @@ __device__ __forceinline__ void tower32w_board(const float* __restrict__ planes,
     }
     for (int b = 0; b < ta.blocks; b++) {
         const unsigned wb3 = b + 1 < ta.blocks ? ta.wwbytes[2 * b + 2] : 0u;   // after the last conv: nothing (reads 0)
+#if defined(AZ_WINO_NOWEIGHTS)   // timing experiment only (wrong results): zero-record descriptors, no weight traffic
+        const __amdgpu_buffer_rsrc_t r1 = t32_rsrc(ta.ww[2 * b], 0), r2 = t32_rsrc(ta.ww[2 * b + 1], 0), r3 = t32_rsrc(ta.ww[0], 0);
+        (void)wb3;
+#elif defined(AZ_WINO_SAMEW)     // timing experiment only (wrong results): every conv streams conv 0's weights
+        const __amdgpu_buffer_rsrc_t r1 = t32_rsrc(ta.ww[0], ta.wwbytes[0]), r2 = r1, r3 = r1;
+        (void)wb3;
+#else
         const __amdgpu_buffer_rsrc_t r1 = t32_rsrc(ta.ww[2 * b], ta.wwbytes[2 * b]);
         const __amdgpu_buffer_rsrc_t r2 = t32_rsrc(ta.ww[2 * b + 1], ta.wwbytes[2 * b + 1]);
         const __amdgpu_buffer_rsrc_t r3 = t32_rsrc(b + 1 < ta.blocks ? ta.ww[2 * b + 2] : ta.ww[2 * b + 1], wb3);
+#endif
         conv_wino<F, false>(ldsb, vbase, r1, r2, ta.b[1 + 2 * b], wring, xres, w, lane);
         conv_wino<F, true>(ldsb, vbase, r2, r3, ta.b[2 + 2 * b], wring, xres, w, lane);
     }

@@ -133,3 +133,55 @@ def test_winograd_tower_matches_direct_tower(require_gpu, blocks, filters, monke
     pd, vd = dn.forward(planes)
     np.testing.assert_allclose(vw, vd, atol=1e-5)
     np.testing.assert_allclose(pw, pd, rtol=1e-4, atol=1e-8)
+
+
+def test_headline_net_many_positions_and_search_rows(require_gpu):
+    """The headline network (20x256 f32, tower32w_kernel<256>) on 64 random-playout positions
+    through AlphaZero::forward, and on the rows the search itself evaluated (search mode: the heads
+    write the priors straight into the new nodes' edges) for 48 games x 3 simulations from random
+    histories -- every row within the f32 tolerance of the oracle network."""
+    B, F = 20, 256
+    w = A.random_weights(B, F, seed=42)
+    net = A.AlphaZero(B, F, weights=w, dtype="f32")
+    ref = O.RefNet(B, F, w)
+    planes = random_planes(64, 2026)
+    pol, val = net.forward(planes)
+    rpol, rval = ref.forward(planes, threads=16)
+    check(pol, val, rpol.astype(np.float64), rval.astype(np.float64), "f32")
+    # search-mode rows
+    rng = np.random.default_rng(9)
+    hs = []
+    while len(hs) < 48:
+        gs, h = A.GameState(), []
+        for _ in range(int(rng.integers(0, 80))):
+            idx = gs.position.legal_indices()
+            a = int(rng.choice(idx))
+            if int(A.play_move(gs, a)) != 0:
+                break
+            h.append(a)
+        else:
+            if len(gs.position.legal_indices()):
+                hs.append(h)
+    s = A.BatchedSearch(net, games=len(hs), sims=3, seed=4, record_evals=True, eval_log_cap=1024, cache_capacity=0)
+    s.set_roots(hs, apply_noise=False)
+    s.run()
+    keys, vals, off, idx, pri = s.eval_log()
+    # the rows evaluated on the roots and on their children (most leaves of a 3-simulation search;
+    # deeper leaves are not looked up)
+    pos = {}
+    for h in hs:
+        p = A.Position.startpos()
+        for a in h:
+            p = p.play(a)
+        pos.setdefault(p.fen_key(), p)
+        for i in np.unique(p.legal_indices()):
+            q = p.play(int(i))
+            pos.setdefault(q.fen_key(), q)
+    rows = [r for r in range(len(keys)) if int(keys[r]) in pos]
+    assert len(rows) >= 64
+    x = np.concatenate([A.to_tensor(pos[int(keys[r])]) for r in rows])
+    rp, rv = ref.forward(x, threads=16)
+    for k, r in enumerate(rows):
+        assert abs(float(vals[r]) - float(rv[k])) <= 1e-5
+        ii = idx[off[r]:off[r + 1]]
+        assert np.all(np.abs(pri[off[r]:off[r + 1]] - rp[k][ii]) <= 1e-4 * rp[k][ii] + 1e-8)
