@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "az_internal.h"
+#include "wino.h"
 
 namespace azi {
 namespace tr {
@@ -466,6 +467,79 @@ loss_kernel(const float* __restrict__ logits, const float* __restrict__ tpol, co
 
 // ------------------------------------------------------------------ weight repacking
 // conv [co][ci][3][3] (burn) -> Wf[t][k][co] (k < kpad, rows >= cin zero) and Wd[t][co][ci] = Wf[8-t]^T
+// ------------------------------------------------------------------ Winograd forward / data grad
+// The 3x3 F -> F convs of the residual tower (F = 256) as Winograd F(2x2, 3x3) -- the inference
+// tower's core (wino.h), 2.25x fewer MFMAs than the implicit GEMM, f32 throughout -- one board
+// per 512-thread workgroup: the board's 64 rows of X into LDS, wino_core, Y (+ addend) back to
+// HBM with no ReLU (BatchNorm runs in training mode after it).  The data grad is the same conv of
+// dY with the flipped, transposed kernel (U built by wino_weights_kernel with flip = 1).
+template <bool ADD>
+__global__ void __launch_bounds__(512)
+conv_wino_train_kernel(const float* __restrict__ X, const uint4* __restrict__ U, unsigned ubytes,
+                       const float* __restrict__ bias, const float* __restrict__ addend, float* __restrict__ Y) {
+    constexpr int F = 256, NN = WinoCfg<F>::NN, XSn = WinoCfg<F>::XS, PF = WinoCfg<F>::PF, RS = F / 4 + 2;
+    constexpr int XSZ = 64 * RS, VSZ = 2 * WinoCfg<F>::CH * 1024 / 16;
+    __shared__ __attribute__((aligned(16))) uint4 lds[XSZ + VSZ];
+    const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const size_t row0 = (size_t)vgpr_index(blockIdx.x) * 64;
+    const uint4* X4 = reinterpret_cast<const uint4*>(X) + row0 * (F / 4);
+    for (int c = tid; c < 64 * (F / 4); c += 512) lds[(c / (F / 4)) * RS + c % (F / 4)] = X4[c];
+    __syncthreads();
+    const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc((void*)U, (short)0, (int)ubytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rN = __builtin_amdgcn_make_buffer_rsrc((void*)U, (short)0, 0, 0x00020000);
+    const int voff = wino_voff<F>(w, lane);
+    f32x4 wr[PF][XSn][NN];
+#pragma unroll
+    for (int i = 0; i < PF; i++)
+#pragma unroll
+        for (int xs = 0; xs < XSn; xs++)
+#pragma unroll
+            for (int n = 0; n < NN; n++)
+                wr[i][xs][n] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                             rW, voff + n * 1024 + wino_toff<F>(0, i * XSn + xs), 0, 0));
+    f32x4 y[NN][4];
+    wino_core<F>(reinterpret_cast<char*>(lds), XSZ * 16, rW, rN, bias, wr, w, lane, y);
+    const int l16 = lane & 15, h = lane >> 4, ty = l16 >> 2, tx = l16 & 3;
+    const int co0 = w * 16 * NN + h * 4;
+#pragma unroll
+    for (int n = 0; n < NN; n++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const size_t o = (row0 + (2 * ty + (q >> 1)) * 8 + 2 * tx + (q & 1)) * F + co0 + n * 16;
+            f32x4 v = y[n][q];
+            if constexpr (ADD) v += *reinterpret_cast<const f32x4*>(addend + o);
+            *reinterpret_cast<f32x4*>(Y + o) = v;
+        }
+}
+
+// Winograd weights U = G g G^T (f64, rounded once to f32: the same arithmetic as net.hip's
+// winograd_f32) of one F x F 3x3 conv in the burn layout w[co][ci][3][3], into the layout
+// wino_core streams ([ci/16][xi][co/16][lane][4]); flip = 1: the data-grad conv's kernel
+// g'[o = ci][i = co][ky][kx] = w[co][ci][2 - ky][2 - kx].  One thread per (output, input) pair.
+__global__ void __launch_bounds__(256) wino_weights_kernel(const float* __restrict__ w, int F, int flip,
+                                                           float* __restrict__ U) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= F * F) return;
+    const int o = idx / F, i = idx % F;      // output / input channel of the conv U describes
+    double g[3][3];
+    for (int ky = 0; ky < 3; ky++)
+        for (int kx = 0; kx < 3; kx++)
+            g[ky][kx] = flip ? (double)w[((size_t)i * F + o) * 9 + (2 - ky) * 3 + (2 - kx)]
+                             : (double)w[((size_t)o * F + i) * 9 + ky * 3 + kx];
+    const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
+    const int CF = F / 16;
+    for (int a = 0; a < 4; a++) {
+        double gg[3];
+        for (int j = 0; j < 3; j++) gg[j] = G[a][0] * g[0][j] + G[a][1] * g[1][j] + G[a][2] * g[2][j];
+        for (int b = 0; b < 4; b++) {
+            const double u = gg[0] * G[b][0] + gg[1] * G[b][1] + gg[2] * G[b][2];
+            const int step = (i / 16) * 16 + a * 4 + b;
+            const int lane = (o % 16) + 16 * ((i % 16) / 4);
+            U[(((size_t)step * CF + o / 16) * 64 + lane) * 4 + i % 4] = (float)u;
+        }
+    }
+}
+
 __global__ void repack3x3_kernel(const float* __restrict__ w, int co_n, int ci_n, int kpad, float* __restrict__ wf,
                                  float* __restrict__ wd) {
     const size_t n = (size_t)9 * kpad * co_n;
@@ -577,6 +651,10 @@ struct Trainer {
     int last_batch = 0;
     // repacked weights
     std::vector<float*> wf, wd;
+    // Winograd weights of the residual convs (F = 256): forward and data grad (env AZ_TRAIN_WINOGRAD=0: off)
+    bool wino = false;
+    std::vector<float*> uf, ud;
+    size_t ubytes = 0;
     float *w40f = nullptr, *w40d = nullptr, *b40 = nullptr, *wp2f = nullptr, *w1d = nullptr;
     // saved activations (R = B*64 rows)
     float* x0 = nullptr;                     // [R][64] input planes
@@ -629,6 +707,17 @@ int launch_conv(Trainer* T, int taps, const float* X, int ldx, int K, const floa
     if (taps == 9) tr::conv_f32_kernel<9><<<grid, 256, 0, T->st>>>(X, ldx, K, W, N, bias, addend, Y, ldy, R);
     else tr::conv_f32_kernel<1><<<grid, 256, 0, T->st>>>(X, ldx, K, W, N, bias, addend, Y, ldy, R);
     return hipGetLastError() == hipSuccess ? 0 : fail("conv launch failed");
+}
+
+// Y = conv3x3(X, U) (+ bias) (+ addend) over B whole boards, Winograd (F = 256 residual convs)
+int launch_wino(Trainer* T, const float* X, const float* U, const float* bias, const float* addend, float* Y, int B) {
+    if (addend)
+        tr::conv_wino_train_kernel<true><<<B, 512, 0, T->st>>>(X, reinterpret_cast<const uint4*>(U), (unsigned)T->ubytes,
+                                                                bias, addend, Y);
+    else
+        tr::conv_wino_train_kernel<false><<<B, 512, 0, T->st>>>(X, reinterpret_cast<const uint4*>(U), (unsigned)T->ubytes,
+                                                                 bias, nullptr, Y);
+    return hipGetLastError() == hipSuccess ? 0 : fail("Winograd conv launch failed");
 }
 
 // dW[taps][K][N] = sum_r X[r+d_t][k] * DY[r][n]
@@ -713,6 +802,11 @@ int trainer_grads(Trainer* T, const float* planes, const float* tpol, const floa
     // weights of this step in GEMM layouts
     for (size_t i = 0; i < L.tower.size(); i++) {
         const auto& c = L.tower[i];
+        if (i > 0 && T->wino) {      // residual convs: Winograd weights, forward and data grad
+            tr::wino_weights_kernel<<<grid_for((size_t)F * F), 256, 0, st>>>(T->p + c.w, F, 0, T->uf[i]);
+            tr::wino_weights_kernel<<<grid_for((size_t)F * F), 256, 0, st>>>(T->p + c.w, F, 1, T->ud[i]);
+            continue;
+        }
         const int kpad = i == 0 ? 64 : F;
         tr::repack3x3_kernel<<<grid_for((size_t)9 * kpad * F), 256, 0, st>>>(T->p + c.w, F, c.cin, kpad, T->wf[i],
                                                                            i == 0 ? nullptr : T->wd[i]);
@@ -738,9 +832,11 @@ int trainer_grads(Trainer* T, const float* planes, const float* tpol, const floa
     for (int b = 0; b < T->blocks; b++) {
         const auto& c1 = L.tower[1 + 2 * b];
         const auto& c2 = L.tower[2 + 2 * b];
-        TRY(launch_conv(T, 9, T->xs[b], F, F, T->wf[1 + 2 * b], F, T->p + c1.b, nullptr, T->y1[b], F, R));
+        if (T->wino) TRY(launch_wino(T, T->xs[b], T->uf[1 + 2 * b], T->p + c1.b, nullptr, T->y1[b], B));
+        else TRY(launch_conv(T, 9, T->xs[b], F, F, T->wf[1 + 2 * b], F, T->p + c1.b, nullptr, T->y1[b], F, R));
         TRY(bn_forward(T, 1 + 2 * b, T->y1[b], F, F, R, c1.bn, nullptr, T->hh[b]));
-        TRY(launch_conv(T, 9, T->hh[b], F, F, T->wf[2 + 2 * b], F, T->p + c2.b, nullptr, T->y2[b], F, R));
+        if (T->wino) TRY(launch_wino(T, T->hh[b], T->uf[2 + 2 * b], T->p + c2.b, nullptr, T->y2[b], B));
+        else TRY(launch_conv(T, 9, T->hh[b], F, F, T->wf[2 + 2 * b], F, T->p + c2.b, nullptr, T->y2[b], F, R));
         TRY(bn_forward(T, 2 + 2 * b, T->y2[b], F, F, R, c2.bn, T->xs[b], T->xs[b + 1]));
     }
     const float* body = T->xs[T->blocks];
@@ -796,12 +892,14 @@ int trainer_grads(Trainer* T, const float* planes, const float* tpol, const floa
         TRY(bias_grad(T, T->dy, F, F, R, T->g + c2.b));
         TRY(launch_wgrad(T, 9, T->hh[b], F, F, T->dy, F, F, R, T->dwtmp, T->dwtmp_cap));
         tr::unpack3x3_kernel<<<grid_for((size_t)9 * F * F), 256, 0, st>>>(T->dwtmp, F, F, F, T->g + c2.w);
-        TRY(launch_conv(T, 9, T->dy, F, F, T->wd[2 + 2 * b], F, nullptr, nullptr, T->dh, F, R));
+        if (T->wino) TRY(launch_wino(T, T->dy, T->ud[2 + 2 * b], nullptr, nullptr, T->dh, B));
+        else TRY(launch_conv(T, 9, T->dy, F, F, T->wd[2 + 2 * b], F, nullptr, nullptr, T->dh, F, R));
         TRY(bn_backward(T, 1 + 2 * b, T->dh, T->hh[b], T->y1[b], F, F, R, c1.bn, T->dy, nullptr));
         TRY(bias_grad(T, T->dy, F, F, R, T->g + c1.b));
         TRY(launch_wgrad(T, 9, T->xs[b], F, F, T->dy, F, F, R, T->dwtmp, T->dwtmp_cap));
         tr::unpack3x3_kernel<<<grid_for((size_t)9 * F * F), 256, 0, st>>>(T->dwtmp, F, F, F, T->g + c1.w);
-        TRY(launch_conv(T, 9, T->dy, F, F, T->wd[1 + 2 * b], F, nullptr, T->dres, T->dxn, F, R));
+        if (T->wino) TRY(launch_wino(T, T->dy, T->ud[1 + 2 * b], nullptr, T->dres, T->dxn, B));
+        else TRY(launch_conv(T, 9, T->dy, F, F, T->wd[1 + 2 * b], F, nullptr, T->dres, T->dxn, F, R));
         std::swap(T->dx, T->dxn);
     }
     // input conv (no data grad)
@@ -900,9 +998,17 @@ int az_trainer_create(int blocks, int filters, const float* weights, size_t n, i
     if (mk) T->allocs.push_back(mk);
     T->mask = reinterpret_cast<uint8_t*>(mk);
     const int nconv = 1 + 2 * blocks;
+    T->wino = F == 256;
+    if (const char* e = getenv("AZ_TRAIN_WINOGRAD")) T->wino = T->wino && atoi(e) != 0;
+    // Winograd U per residual conv: 16 points x F x F + 8 zero ring steps of prefetch pad
+    const size_t ufl = (size_t)16 * F * F + (size_t)8 * (F / 16) * 64 * 4;
+    T->ubytes = ufl * sizeof(float);
     for (int i = 0; i < nconv; i++) {
-        T->wf.push_back(A((size_t)9 * (i == 0 ? 64 : F) * F));
-        T->wd.push_back(i == 0 ? nullptr : A((size_t)9 * F * F));
+        const bool w9 = i == 0 || !T->wino;
+        T->wf.push_back(w9 ? A((size_t)9 * (i == 0 ? 64 : F) * F) : nullptr);
+        T->wd.push_back(i == 0 || !w9 ? nullptr : A((size_t)9 * F * F));
+        T->uf.push_back(i > 0 && T->wino ? A(ufl) : nullptr);
+        T->ud.push_back(i > 0 && T->wino ? A(ufl) : nullptr);
     }
     T->w40f = A((size_t)F * 64); T->w40d = A((size_t)64 * F); T->b40 = A(64); T->wp2f = A(32 * 64); T->w1d = A(64 * 512);
     T->x0 = A(R * 64);
@@ -955,6 +1061,14 @@ int az_trainer_create(int blocks, int filters, const float* weights, size_t n, i
         hipMemset(T->g, 0, T->np * sizeof(float)) != hipSuccess) {
         delete T;
         return fail("az_trainer_create: upload failed");
+    }
+    // the Winograd weight buffers' prefetch pad stays zero (the per-step transforms write the rest)
+    for (size_t i = 0; i < T->uf.size(); i++) {
+        if (!T->uf[i]) continue;
+        if (hipMemset(T->uf[i], 0, T->ubytes) != hipSuccess || hipMemset(T->ud[i], 0, T->ubytes) != hipSuccess) {
+            delete T;
+            return fail("az_trainer_create: upload failed");
+        }
     }
     *out = new az_trainer{T};
     return 0;

@@ -1,0 +1,283 @@
+// wino.h -- the f32 Winograd F(2x2, 3x3) conv of one board, shared by the inference tower
+// (tower.hip: tower32w_kernel, k_sims32w) and the training step (train.hip: conv_wino_train_kernel).
+#pragma once
+#include "az_internal.h"
+
+namespace azi {
+
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+// ====================================================================== f32 Winograd tower
+// tower32w_kernel: the same f32 tower with every residual 3x3 conv as Winograd F(2x2, 3x3)
+// (Lavin & Gray): the 8x8 board is 16 output tiles of 2x2 whose 4x4 input patches are
+// transformed V = B^T d B (16 points xi), the weights were transformed on the host
+// U = G g G^T (f64, rounded once to f32), M[xi] = U[xi] V[xi] summed over the input channels is
+// 16 GEMMs of F x 16 tiles x F on v_mfma_f32_16x16x4_f32 (exact f32 products), and
+// Y = A^T M A.  2.25x fewer MFMAs than the direct conv (16 tiles x 16 points vs 64 squares x 9
+// taps).  Numerics: f32 throughout; the transforms' rounding adds ~1.3x the direct f32 error
+// (numpy check), checked against the oracle within the f32 tolerance.
+// One board per workgroup:
+//   ACT [64 squares][F/4 + 2 slots] f32 in LDS -- the layer input, overwritten in place by the
+//       output (the block input x stays in the registers of the wave that owns it, as the residual);
+//   V   [16 xi][channel quads][16 tiles][4] f32 in CH-channel chunks (double-buffered when the
+//       input takes more than one chunk): chunk c+1 is transformed by all waves, one (channel,
+//       tile) item per thread, while the MFMAs of chunk c run; one barrier per chunk;
+//   weights [F/16 ci groups][16 xi][F/16 co groups][64 lanes][4] f32 per conv, streamed from L2
+//       through a register ring of PF steps that carries across layers.
+// Step constants (C3 / C2 A/B logs: profiles/r02_ab_wino_s9_knobs_c3.log, r02_ab_wino64_*):
+//   WINO_TSPLIT 2  steps between a chunk's patch reads and their transform + V writes (8 -> 2: -2 %)
+//   WINO_TSTAG 16  steps by which the second wave of each SIMD pair delays its transform (-0.4 %)
+//   WINO_LA 4      B fragments read ahead from V
+constexpr int WINO_TSPLIT = 2, WINO_TSTAG = 16, WINO_LA = 4;
+
+// Per filter count: NWV waves per workgroup, NN 16-channel output fragments per wave, XS points
+// per ring step, CH input channels per transform chunk (V buffer = CH KB), PF ring steps of
+// weight prefetch.  Every wave owns NN output fragments x all 16 points.
+//   F = 256: 8 waves (two per SIMD) x 32 output channels, one point per step (two independent
+//            accumulator chains per step), 32-channel chunks;
+//   F = 128: 8 waves x 16 channels, two points per step (still two chains: the f32 MFMA's
+//            dependent latency exceeds its issue interval);
+//   F = 64:  4 waves (one per SIMD) x 16 channels, two points per step, the whole 64-channel input
+//            transformed as one chunk (one transform phase and one barrier per conv: C2 A/B -8 %).
+template <int F> struct WinoCfg;
+template <> struct WinoCfg<256> { static constexpr int NWV = 8, NN = 2, XS = 1, CH = 32, PF = 2; };
+template <> struct WinoCfg<128> { static constexpr int NWV = 8, NN = 1, XS = 2, CH = 32, PF = 2; };
+template <> struct WinoCfg<64> { static constexpr int NWV = 4, NN = 1, XS = 2, CH = 64, PF = 2; };
+// Winograd weight fragment offsets: wave w's lane base (output fragments NN w..) and the byte
+// offset of ring step t (16-channel group kl = t / 16, point t % 16) of chunk cg
+template <int F> __device__ __forceinline__ int wino_voff(int w, int lane) {
+    return (WinoCfg<F>::NN * w * 64 + lane) * 16;
+}
+template <int F> __device__ __forceinline__ int wino_toff(int cg, int t) {
+    constexpr int KPC = WinoCfg<F>::CH / 16, CF = F / 16;
+    return ((cg * KPC + t / 16) * 16 + t % 16) * CF * 1024;
+}
+
+// wino_core: one Winograd conv of the board whose layer input is in ACT ([64 squares][F/4 + 2
+// slots] f32 at ldsb), V buffers at vbase: every wave's y[n][q] = this wave's outputs (output
+// fragment n, tile lane & 15, square (2 ty + q / 2, 2 tx + q % 2), channels co0 + 16 n + 0..3)
+// + bias (nullptr: none).  Ends after the last chunk's barrier: every wave has finished reading
+// ACT and V, so the caller may overwrite them.
+// wr: the weight ring; holds this conv's first PF steps on entry and the next conv's (rN) on
+// exit, so no layer starts on a cold weight fetch
+template <int F>
+__device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
+                                          const __amdgpu_buffer_rsrc_t rW, const __amdgpu_buffer_rsrc_t rN,
+                                          const float* __restrict__ bias,
+                                          f32x4 (&wr)[WinoCfg<F>::PF][WinoCfg<F>::XS][WinoCfg<F>::NN], int w,
+                                          int lane, f32x4 (&y)[WinoCfg<F>::NN][4]) {
+    constexpr int CF = F / 16, RS = F / 4 + 2;
+    constexpr int NWV = WinoCfg<F>::NWV, NN = WinoCfg<F>::NN, XS = WinoCfg<F>::XS;
+    constexpr int CH = WinoCfg<F>::CH, VBYTES = CH * 1024, XST = CH * 64;   // V buffer, xi stride
+    constexpr int IT = CH * 16 / (NWV * 64);                       // transform items per thread per chunk
+    // t = (16-channel group kl, point t % 16) pairs of this wave per chunk; a ring step covers XS
+    constexpr int NCHUNK = F / CH, KPC = CH / 16, SPC = KPC * 16, SPX = SPC / XS;
+    constexpr int PF = WinoCfg<F>::PF, LA = WINO_LA * XS;
+    static_assert(NN * 16 * NWV == F && IT * NWV * 64 == CH * 16 && NWV % 4 == 0 && IT >= 1, "Winograd config");
+    static_assert(SPX % PF == 0 && SPC % LA == 0 && 16 % XS == 0, "ring slots must be compile-time");
+    const int l16 = lane & 15, h = lane >> 4;
+    // V[xi][quad cq][tile slot][4]: tile slot = tile ^ 2 (cq & 3).  gfx950 services a ds_read_b128
+    // in the lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31} (+32): each group holds quads h and
+    // h + 1 of a fragment at complementary tile sets, and the XOR by 2h keeps their 16 slots distinct
+    // (64 banks); a ds_write_b32 of the transform (32-lane groups, 32 banks) then covers 8 distinct
+    // slot values mod 8, so both are conflict-free (an XOR by 4h, laid out for groups of 16
+    // consecutive lanes, made every B-fragment read 2-way: PMC 48 % of LDS cycles were conflicts)
+    const int vrd = h * 256 + ((l16 ^ (2 * h)) * 16);               // + xi * XST + k * 1024 (cq = 4k + h, cq & 3 = h)
+    // transform items: wave w covers tile row ty = w & 3 and 16 channels per item: channel
+    // 16 (w >> 2 + it NWV / 4) + (lane & 15) of the chunk, tile (w & 3, lane >> 4) -- a patch read
+    // then touches 4 tiles of one row x 16 consecutive channels: conflict-free with the ACT row
+    // stride of 8 banks mod 64
+    const int tty = w & 3, ttx = lane >> 4;
+    auto tchan = [&](int it) { return 16 * ((w >> 2) + it * (NWV / 4)) + (lane & 15); };
+    auto vwr = [&](int tch) {   // + xi * XST
+        return (tch >> 2) * 256 + (((4 * tty + ttx) ^ (2 * ((tch >> 2) & 3))) * 16) + (tch & 3) * 4;
+    };
+    // V[buf] <- B^T d B of chunk c for this thread's item, in two halves: tload issues the patch
+    // reads, tstore (WINO_TSPLIT steps later, their latency hidden behind MFMAs) transforms and writes
+    auto tload = [&](int c, float (&d)[IT][4][4]) {
+        // patch addresses recomputed per chunk from a laundered index: hoisted out of the chunk
+        // loop they were 16 loop-invariant registers, and spilled
+        const int tl = vgpr_index(ttx);
+        // element (i, j) of the patch is square (2 tty - 1 + i, 2 tl - 1 + j): the row part is
+        // wave-uniform (tty = w & 3), so every address is a per-column lane base + a row offset
+        // that is an instruction immediate (row 1) or one scalar add (rows 0, 2, 3, clamped onto
+        // the board when they fall off it); off-board elements are read at an on-board square and
+        // zeroed afterwards (row: wave-uniform select, column: lane select)
+        constexpr int R16 = RS * 16;
+        const int rowb1 = (2 * tty) * 8 * R16;                              // row i = 1
+        const int d0 = tty > 0 ? -8 * R16 : 0, d3 = tty < 3 ? 16 * R16 : 8 * R16;
+        // row 2's offset as an opaque scalar: as an immediate the compiler pairs rows 1 and 2 into
+        // ds_read2st64_b32 and then moves the pairs apart, waiting for the reads on the spot
+        // (s_waitcnt in the step that issues them) instead of steps later in tstore
+        const int d2 = __builtin_amdgcn_readfirstlane(vgpr_index(8 * R16));
+        const bool c0ok = tl > 0, c3ok = tl < 3;
+        // the clamped columns (3, 4) keep the 32-lane groups of each ds_read_b32 on distinct banks
+        const int cs0 = c0ok ? 2 * tl - 1 : 3, cs3 = c3ok ? 2 * tl + 2 : 4;
+#pragma unroll
+        for (int it = 0; it < IT; it++) {
+            const int chan = (c * CH + tchan(it)) * 4 + rowb1;
+            const int cb[4] = {cs0 * R16 + chan, 2 * tl * R16 + chan, (2 * tl + 1) * R16 + chan, cs3 * R16 + chan};
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                d[it][0][j] = *reinterpret_cast<const float*>(ldsb + cb[j] + d0);
+                d[it][1][j] = *reinterpret_cast<const float*>(ldsb + cb[j]);
+                d[it][2][j] = *reinterpret_cast<const float*>(ldsb + cb[j] + d2);
+                d[it][3][j] = *reinterpret_cast<const float*>(ldsb + cb[j] + d3);
+            }
+        }
+    };
+    auto tstore = [&](int buf, const float (&d)[IT][4][4]) {
+        const int tl = vgpr_index(ttx);
+#pragma unroll
+        for (int it = 0; it < IT; it++) {
+            float e[4][4];
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    e[i][j] = d[it][i][j];
+                    // zero the off-board elements tload read at clamped squares
+                    if ((i == 0 && tty == 0) || (i == 3 && tty == 3)) e[i][j] = 0.f;
+                    if (j == 0) e[i][j] = tl > 0 ? e[i][j] : 0.f;
+                    if (j == 3) e[i][j] = tl < 3 ? e[i][j] : 0.f;
+                }
+            float tt[4][4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                tt[0][j] = e[0][j] - e[2][j];
+                tt[1][j] = e[1][j] + e[2][j];
+                tt[2][j] = e[2][j] - e[1][j];
+                tt[3][j] = e[1][j] - e[3][j];
+            }
+            char* vb = ldsb + vbase + buf * VBYTES + vwr(tchan(it));
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const float v0 = tt[r][0] - tt[r][2], v1 = tt[r][1] + tt[r][2], v2 = tt[r][2] - tt[r][1], v3 = tt[r][1] - tt[r][3];
+                *reinterpret_cast<float*>(vb + (r * 4 + 0) * XST) = v0;
+                *reinterpret_cast<float*>(vb + (r * 4 + 1) * XST) = v1;
+                *reinterpret_cast<float*>(vb + (r * 4 + 2) * XST) = v2;
+                *reinterpret_cast<float*>(vb + (r * 4 + 3) * XST) = v3;
+            }
+        }
+    };
+    const int co0 = w * 16 * NN + h * 4;
+    f32x4 acc[16][NN];
+#pragma unroll
+    for (int x = 0; x < 16; x++)
+#pragma unroll
+        for (int n = 0; n < NN; n++) acc[x][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // weight ring: fragment (16-channel group kc, point xi, co/16 = NN w + n) at ((kc 16 + xi) CF + co/16) KB
+    const int voff = wino_voff<F>(w, lane);
+    {
+        float d0[IT][4][4];
+        tload(0, d0);
+        tstore(0, d0);
+    }
+    __syncthreads();
+    // B fragment of this wave's step t: 16-channel group t / 16 of the chunk, point t % 16
+    auto boff = [](int t) { return (t / 16) * 1024 + (t % 16) * XST; };
+#ifdef AZ_WINO_NOBAR   // timing experiment only (wrong results): no chunk barrier, B read-ahead across chunks
+    f32x4 bq[LA];
+#pragma unroll
+    for (int i = 0; i < LA; i++) bq[i] = *reinterpret_cast<const f32x4*>(ldsb + vbase + vrd + boff(i));
+#endif
+#pragma unroll 1
+    for (int c = 0; c < NCHUNK; c++) {
+        float dn[IT][4][4];
+        const int vb = vbase + (c & 1) * VBYTES + vrd;
+        const bool more = c + 1 < NCHUNK;
+#ifndef AZ_WINO_NOBAR
+        f32x4 bq[LA];
+#pragma unroll
+        for (int i = 0; i < LA; i++) bq[i] = *reinterpret_cast<const f32x4*>(ldsb + vb + boff(i));
+#endif
+#pragma unroll
+        for (int st = 0; st < SPX; st++) {
+            f32x4 B[XS];
+#pragma unroll
+            for (int xs = 0; xs < XS; xs++) {
+                const int t = st * XS + xs;
+                B[xs] = bq[t % LA];
+                if (t + LA < SPC) bq[t % LA] = *reinterpret_cast<const f32x4*>(ldsb + vb + boff(t + LA));
+#ifdef AZ_WINO_NOBAR
+                else if (more) bq[t % LA] = *reinterpret_cast<const f32x4*>(ldsb + vbase + ((c + 1) & 1) * VBYTES + vrd + boff(t + LA - SPC));
+#endif
+            }
+            f32x4 a[XS][NN];
+#pragma unroll
+            for (int xs = 0; xs < XS; xs++)
+#pragma unroll
+                for (int n = 0; n < NN; n++) a[xs][n] = wr[st % PF][xs][n];
+            {
+                // ring step st + PF: the steps of a conv are linear in the weights; past this
+                // conv's last step the refills read the next conv's first steps
+                const int cadd = (st + PF) / SPX;
+                const bool nxt = cadd > 0 && !more;
+                const int tn = c * SPX + st + PF;
+                const int to = (nxt ? tn - NCHUNK * SPX : tn) * XS;
+#pragma unroll
+                for (int xs = 0; xs < XS; xs++)
+#pragma unroll
+                    for (int n = 0; n < NN; n++)
+                        wr[st % PF][xs][n] = __builtin_bit_cast(
+                            f32x4, __builtin_amdgcn_raw_buffer_load_b128(nxt ? rN : rW,
+                                                                         voff + n * 1024 + (to + xs) * CF * 1024, 0, 0));
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int s4 = 0; s4 < 4; s4++)
+#pragma unroll
+                for (int xs = 0; xs < XS; xs++)
+#pragma unroll
+                    for (int n = 0; n < NN; n++) {
+                        const int x = (st * XS + xs) % 16;
+                        acc[x][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[xs][n][s4], B[xs][s4], acc[x][n], 0, 0, 0);
+                    }
+            __builtin_amdgcn_sched_barrier(0);
+            // the next chunk's transform; the two waves of a SIMD pair run their transform VALU
+            // blocks at different steps, so that one of them keeps the matrix pipe busy (a stagger
+            // that would not fit in this F's chunk is dropped)
+            constexpr int TSG = (WINO_TSTAG + WINO_TSPLIT) / XS < SPX ? WINO_TSTAG : 0;
+            if constexpr (TSG == 0) {
+                if (st == 0 && more) tload(c + 1, dn);
+                if (st == WINO_TSPLIT / XS && more) tstore((c + 1) & 1, dn);
+            } else {
+                const bool late = w >= NWV / 2;
+                if (st == 0 && more && !late) tload(c + 1, dn);
+                if (st == TSG / XS && more && late) tload(c + 1, dn);
+                if (st == WINO_TSPLIT / XS && more && !late) tstore((c + 1) & 1, dn);
+                if (st == (TSG + WINO_TSPLIT) / XS && more && late) tstore((c + 1) & 1, dn);
+            }
+        }
+#ifndef AZ_WINO_NOBAR
+        __syncthreads();
+#endif
+    }
+#ifdef AZ_WINO_NOBAR
+    __syncthreads();
+#endif
+    // output transform Y = A^T M A per (output fragment n, channel r), + bias
+#pragma unroll
+    for (int n = 0; n < NN; n++) {
+        const float4 bb = bias ? *reinterpret_cast<const float4*>(bias + co0 + n * 16) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            float m[4][4];
+#pragma unroll
+            for (int x = 0; x < 16; x++) m[x >> 2][x & 3] = acc[x][n][r];
+            float s0[4], s1[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                s0[j] = m[0][j] + m[1][j] + m[2][j];
+                s1[j] = m[1][j] - m[2][j] - m[3][j];
+            }
+            const float br = r == 0 ? bb.x : r == 1 ? bb.y : r == 2 ? bb.z : bb.w;
+            y[n][0][r] = (s0[0] + s0[1] + s0[2]) + br;
+            y[n][1][r] = (s0[1] - s0[2] - s0[3]) + br;
+            y[n][2][r] = (s1[0] + s1[1] + s1[2]) + br;
+            y[n][3][r] = (s1[1] - s1[2] - s1[3]) + br;
+        }
+    }
+}
+
+}  // namespace azi
