@@ -853,18 +853,24 @@ __device__ __forceinline__ void tower32w_board(const float* __restrict__ planes,
     constexpr int VSZ = (F / WinoCfg<F>::CH > 1 ? 2 : 1) * WinoCfg<F>::CH * 1024 / 16;
     constexpr int PF = WinoCfg<F>::PF;
     constexpr int ZN = 16 + F / 4;
+    constexpr int PAD = WINO_PAD_SQ * RSF;               // zero squares either side of ACT
     static_assert(HeadsScratch<1, NT, heads_npart(NT, true)>::FLOATS * 4 <= VSZ * 16, "heads scratch must fit in V");
     static_assert(64 * RSI <= VSZ, "input planes must fit in V");
-    __shared__ __attribute__((aligned(16))) uint4 lds[XSZ + VSZ + ZN];
+    __shared__ __attribute__((aligned(16))) uint4 lds[PAD + XSZ + PAD + VSZ + ZN];
     const int lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    uint4* X = lds;
-    uint4* V = lds + XSZ;
-    const int vbase = XSZ * 16;
-    const int zero_off = (XSZ + VSZ) * 16;
-    char* ldsb = reinterpret_cast<char*>(lds);
+    uint4* X = lds + PAD;
+    uint4* V = X + XSZ + PAD;
+    const int vbase = (XSZ + PAD) * 16;                  // offsets from ACT
+    const int zero_off = (XSZ + PAD + VSZ) * 16;
+    static_assert((XSZ + PAD + VSZ) * 16 % 256 == 0, "conv32_lds ORs the zero row's offset into the low byte");
+    char* ldsb = reinterpret_cast<char*>(X);
     stage_planes_f32<1, RSI, NT>(V, planes, so, row0, 1, tid);
-    for (int c = tid; c < ZN; c += NT) lds[XSZ + VSZ + c] = make_uint4(0, 0, 0, 0);
+    for (int c = tid; c < ZN; c += NT) V[VSZ + c] = make_uint4(0, 0, 0, 0);
+    for (int c = tid; c < PAD; c += NT) {
+        lds[c] = make_uint4(0, 0, 0, 0);
+        X[XSZ + c] = make_uint4(0, 0, 0, 0);
+    }
     __syncthreads();
     {   // input conv 19 (32) -> F: direct (18 k-steps)
         f32x4 wr[T32_PF][NN];

@@ -478,12 +478,17 @@ __global__ void __launch_bounds__(512)
 conv_wino_train_kernel(const float* __restrict__ X, const uint4* __restrict__ U, unsigned ubytes,
                        const float* __restrict__ bias, const float* __restrict__ addend, float* __restrict__ Y) {
     constexpr int F = 256, NN = WinoCfg<F>::NN, XSn = WinoCfg<F>::XS, PF = WinoCfg<F>::PF, RS = F / 4 + 2;
-    constexpr int XSZ = 64 * RS, VSZ = 2 * WinoCfg<F>::CH * 1024 / 16;
-    __shared__ __attribute__((aligned(16))) uint4 lds[XSZ + VSZ];
+    constexpr int XSZ = 64 * RS, VSZ = 2 * WinoCfg<F>::CH * 1024 / 16, PAD = WINO_PAD_SQ * RS;
+    __shared__ __attribute__((aligned(16))) uint4 lds[PAD + XSZ + PAD + VSZ];
+    uint4* act = lds + PAD;                              // zero squares either side (wino_core)
     const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const size_t row0 = (size_t)vgpr_index(blockIdx.x) * 64;
     const uint4* X4 = reinterpret_cast<const uint4*>(X) + row0 * (F / 4);
-    for (int c = tid; c < 64 * (F / 4); c += 512) lds[(c / (F / 4)) * RS + c % (F / 4)] = X4[c];
+    for (int c = tid; c < 64 * (F / 4); c += 512) act[(c / (F / 4)) * RS + c % (F / 4)] = X4[c];
+    for (int c = tid; c < PAD; c += 512) {
+        lds[c] = make_uint4(0, 0, 0, 0);
+        act[XSZ + c] = make_uint4(0, 0, 0, 0);
+    }
     __syncthreads();
     const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc((void*)U, (short)0, (int)ubytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rN = __builtin_amdgcn_make_buffer_rsrc((void*)U, (short)0, 0, 0x00020000);
@@ -498,7 +503,7 @@ conv_wino_train_kernel(const float* __restrict__ X, const uint4* __restrict__ U,
                 wr[i][xs][n] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                                              rW, voff + n * 1024 + wino_toff<F>(0, i * XSn + xs), 0, 0));
     f32x4 y[NN][4];
-    wino_core<F>(reinterpret_cast<char*>(lds), XSZ * 16, rW, rN, bias, wr, w, lane, y);
+    wino_core<F>(reinterpret_cast<char*>(act), (XSZ + PAD) * 16, rW, rN, bias, wr, w, lane, y);
     const int l16 = lane & 15, h = lane >> 4, ty = l16 >> 2, tx = l16 & 3;
     const int co0 = w * 16 * NN + h * 4;
 #pragma unroll

@@ -6,6 +6,40 @@
 namespace azi {
 
 typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+
+// Packed f32 adds (v_pk_add_f32 / v_pk_fma_f32: two results per VALU issue) with the per-half source
+// selects and negations written out.  Left to itself the compiler packed the transforms' adds but
+// moved operands into register pairs first (one v_mov per packed add), and VALU issue is what the
+// f32 MFMA pipe does not hide.  No memory operands: the waits stay the compiler's.
+#define AZ_PK2(name, mods)                                                                    \
+    __device__ __forceinline__ f32x2 name(f32x2 a, f32x2 b) {                                 \
+        f32x2 r;                                                                              \
+        asm("v_pk_add_f32 %0, %1, %2 " mods : "=v"(r) : "v"(a), "v"(b));                      \
+        return r;                                                                             \
+    }
+#define AZ_PK3(name, mods)                                                                    \
+    __device__ __forceinline__ f32x2 name(f32x2 a, f32x2 m, f32x2 b) {                        \
+        f32x2 r;                                                                              \
+        asm("v_pk_fma_f32 %0, %1, %2, %3 " mods : "=v"(r) : "v"(a), "v"(m), "v"(b));          \
+        return r;                                                                             \
+    }
+AZ_PK2(pk_add, "")                                             // (a.x + b.x, a.y + b.y)
+AZ_PK2(pk_sub, "neg_lo:[0,1] neg_hi:[0,1]")                    // (a.x - b.x, a.y - b.y)
+AZ_PK2(pk_rowa, "op_sel_hi:[1,0] neg_lo:[0,1]")                // (a.x - b.x, a.y + b.x)
+AZ_PK2(pk_rowb, "op_sel:[1,0] neg_lo:[0,1] neg_hi:[0,1]")      // (a.y - b.x, a.y - b.y)
+AZ_PK2(pk_negx_add, "neg_lo:[1,1]")                            // (-a.x - b.x, a.y + b.y)
+AZ_PK2(pk_negx_sub, "neg_lo:[1,0] neg_hi:[0,1]")               // (-a.x + b.x, a.y - b.y)
+AZ_PK3(pk_fma_m0_sub, "op_sel_hi:[1,0,1] neg_lo:[0,0,1] neg_hi:[0,0,1]")    // (a.x m.x - b.x, a.y m.x - b.y)
+AZ_PK3(pk_sub_m3, "op_sel:[0,1,0] neg_lo:[1,0,0] neg_hi:[1,0,0]")          // (b.x - a.x m.y, b.y - a.y m.y)
+AZ_PK3(pk_negx_fma_m0, "op_sel_hi:[1,0,1] neg_lo:[1,0,0] neg_hi:[0,0,1]")   // (-a.x m.x + b.x, a.y m.x - b.y)
+AZ_PK3(pk_negx_sub_m3, "op_sel:[0,1,0] neg_lo:[0,0,1] neg_hi:[1,0,0]")      // (a.x m.y - b.x, -a.y m.y + b.y)
+#undef AZ_PK2
+#undef AZ_PK3
+
+// zero squares before and after ACT ([64 squares][F/4 + 2 slots]): the transform reads the rows
+// above / below the board there
+constexpr int WINO_PAD_SQ = 8;
 
 // ====================================================================== f32 Winograd tower
 // tower32w_kernel: the same f32 tower with every residual 3x3 conv as Winograd F(2x2, 3x3)
@@ -18,7 +52,8 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 // (numpy check), checked against the oracle within the f32 tolerance.
 // One board per workgroup:
 //   ACT [64 squares][F/4 + 2 slots] f32 in LDS -- the layer input, overwritten in place by the
-//       output (the block input x stays in the registers of the wave that owns it, as the residual);
+//       output (the block input x stays in the registers of the wave that owns it, as the residual),
+//       with WINO_PAD_SQ zero squares before and after it;
 //   V   [16 xi][channel quads][16 tiles][4] f32 in CH-channel chunks (double-buffered when the
 //       input takes more than one chunk): chunk c+1 is transformed by all waves, one (channel,
 //       tile) item per thread, while the MFMAs of chunk c run; one barrier per chunk;
@@ -54,7 +89,7 @@ template <int F> __device__ __forceinline__ int wino_toff(int cg, int t) {
 }
 
 // wino_core: one Winograd conv of the board whose layer input is in ACT ([64 squares][F/4 + 2
-// slots] f32 at ldsb), V buffers at vbase: every wave's y[n][q] = this wave's outputs (output
+// slots] f32 at ldsb, WINO_PAD_SQ zero squares on either side), V buffers at vbase: every wave's y[n][q] = this wave's outputs (output
 // fragment n, tile lane & 15, square (2 ty + q / 2, 2 tx + q % 2), channels co0 + 16 n + 0..3)
 // + bias (nullptr: none).  Ends after the last chunk's barrier: every wave has finished reading
 // ACT and V, so the caller may overwrite them.
@@ -94,73 +129,65 @@ __device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
     };
     // V[buf] <- B^T d B of chunk c for this thread's item, in two halves: tload issues the patch
     // reads, tstore (WINO_TSPLIT steps later, their latency hidden behind MFMAs) transforms and writes
-    auto tload = [&](int c, float (&d)[IT][4][4]) {
+    // V[buf] <- B^T d B of chunk c for this thread's item, in two halves: tload issues the patch
+    // reads, tstore (WINO_TSPLIT steps later, their latency hidden behind MFMAs) transforms and writes.
+    // d[it][j] = patch column j as row pairs {rows 0, 1}, {rows 2, 3} (one ds_read2st64_b32 each).
+    auto tload = [&](int c, f32x2 (&d)[IT][4][2]) {
         // patch addresses recomputed per chunk from a laundered index: hoisted out of the chunk
-        // loop they were 16 loop-invariant registers, and spilled
+        // loop they were loop-invariant registers, and spilled
         const int tl = vgpr_index(ttx);
-        // element (i, j) of the patch is square (2 tty - 1 + i, 2 tl - 1 + j): the row part is
-        // wave-uniform (tty = w & 3), so every address is a per-column lane base + a row offset
-        // that is an instruction immediate (row 1) or one scalar add (rows 0, 2, 3, clamped onto
-        // the board when they fall off it); off-board elements are read at an on-board square and
-        // zeroed afterwards (row: wave-uniform select, column: lane select)
-        constexpr int R16 = RS * 16;
-        const int rowb1 = (2 * tty) * 8 * R16;                              // row i = 1
-        const int d0 = tty > 0 ? -8 * R16 : 0, d3 = tty < 3 ? 16 * R16 : 8 * R16;
-        // row 2's offset as an opaque scalar: as an immediate the compiler pairs rows 1 and 2 into
-        // ds_read2st64_b32 and then moves the pairs apart, waiting for the reads on the spot
-        // (s_waitcnt in the step that issues them) instead of steps later in tstore
-        const int d2 = __builtin_amdgcn_readfirstlane(vgpr_index(8 * R16));
-        const bool c0ok = tl > 0, c3ok = tl < 3;
-        // the clamped columns (3, 4) keep the 32-lane groups of each ds_read_b32 on distinct banks
-        const int cs0 = c0ok ? 2 * tl - 1 : 3, cs3 = c3ok ? 2 * tl + 2 : 4;
+        // element (i, j) of the patch is square (2 tty - 1 + i, 2 tl - 1 + j): rows off the board
+        // fall in the zero squares before / after ACT (WINO_PAD_SQ), so every row offset is an
+        // instruction immediate; the off-board columns (tl = 0: j = 0, tl = 3: j = 3) are read at a
+        // clamped on-board column (3 / 4: keeps the 32-lane groups of each read on distinct banks)
+        // and multiplied by 0 in tstore
+        constexpr int R16 = RS * 16, ROW = 8 * R16;
+        const int cs0 = tl > 0 ? 2 * tl - 1 : 3, cs3 = tl < 3 ? 2 * tl + 2 : 4;
 #pragma unroll
         for (int it = 0; it < IT; it++) {
-            const int chan = (c * CH + tchan(it)) * 4 + rowb1;
-            const int cb[4] = {cs0 * R16 + chan, 2 * tl * R16 + chan, (2 * tl + 1) * R16 + chan, cs3 * R16 + chan};
+            const int base = (2 * tty - 1) * ROW + (c * CH + tchan(it)) * 4;
+            const int cb[4] = {base + cs0 * R16, base + 2 * tl * R16, base + (2 * tl + 1) * R16, base + cs3 * R16};
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                d[it][0][j] = *reinterpret_cast<const float*>(ldsb + cb[j] + d0);
-                d[it][1][j] = *reinterpret_cast<const float*>(ldsb + cb[j]);
-                d[it][2][j] = *reinterpret_cast<const float*>(ldsb + cb[j] + d2);
-                d[it][3][j] = *reinterpret_cast<const float*>(ldsb + cb[j] + d3);
+                const char* p = ldsb + cb[j];
+                d[it][j][0] = f32x2{*reinterpret_cast<const float*>(p), *reinterpret_cast<const float*>(p + ROW)};
+                d[it][j][1] = f32x2{*reinterpret_cast<const float*>(p + 2 * ROW), *reinterpret_cast<const float*>(p + 3 * ROW)};
             }
         }
     };
-    auto tstore = [&](int buf, const float (&d)[IT][4][4]) {
+    auto tstore = [&](int buf, const f32x2 (&d)[IT][4][2]) {
         const int tl = vgpr_index(ttx);
+        // (m0, m3): 0 where patch column 0 / 3 is off the board
+        const f32x2 m = f32x2{tl > 0 ? 1.0f : 0.0f, tl < 3 ? 1.0f : 0.0f};
 #pragma unroll
         for (int it = 0; it < IT; it++) {
-            float e[4][4];
-#pragma unroll
-            for (int i = 0; i < 4; i++)
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    e[i][j] = d[it][i][j];
-                    // zero the off-board elements tload read at clamped squares
-                    if ((i == 0 && tty == 0) || (i == 3 && tty == 3)) e[i][j] = 0.f;
-                    if (j == 0) e[i][j] = tl > 0 ? e[i][j] : 0.f;
-                    if (j == 3) e[i][j] = tl < 3 ? e[i][j] : 0.f;
-                }
-            float tt[4][4];
+            // rows: A[j] = (tt0, tt1) = (e0 - e2, e1 + e2), B[j] = (-tt2, tt3) = (e1 - e2, e1 - e3)
+            f32x2 A[4], B[4];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                tt[0][j] = e[0][j] - e[2][j];
-                tt[1][j] = e[1][j] + e[2][j];
-                tt[2][j] = e[2][j] - e[1][j];
-                tt[3][j] = e[1][j] - e[3][j];
+                A[j] = pk_rowa(d[it][j][0], d[it][j][1]);
+                B[j] = pk_rowb(d[it][j][0], d[it][j][1]);
             }
+            // columns, two rows at a time: v0 = t0 m0 - t2, v1 = t1 + t2, v2 = t2 - t1, v3 = t1 - t3 m3
+            // (the same roundings as the scalar form: every multiply is by 1 or 0)
+            const f32x2 a0 = pk_fma_m0_sub(A[0], m, A[2]), a1 = pk_add(A[1], A[2]);
+            const f32x2 a2 = pk_sub(A[2], A[1]), a3 = pk_sub_m3(A[3], m, A[1]);
+            const f32x2 b0 = pk_negx_fma_m0(B[0], m, B[2]), b1 = pk_negx_add(B[1], B[2]);
+            const f32x2 b2 = pk_negx_sub(B[2], B[1]), b3 = pk_negx_sub_m3(B[3], m, B[1]);
             char* vb = ldsb + vbase + buf * VBYTES + vwr(tchan(it));
+            const f32x2 v[4][2] = {{a0, b0}, {a1, b1}, {a2, b2}, {a3, b3}};   // [column k][row pair]
 #pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const float v0 = tt[r][0] - tt[r][2], v1 = tt[r][1] + tt[r][2], v2 = tt[r][2] - tt[r][1], v3 = tt[r][1] - tt[r][3];
-                *reinterpret_cast<float*>(vb + (r * 4 + 0) * XST) = v0;
-                *reinterpret_cast<float*>(vb + (r * 4 + 1) * XST) = v1;
-                *reinterpret_cast<float*>(vb + (r * 4 + 2) * XST) = v2;
-                *reinterpret_cast<float*>(vb + (r * 4 + 3) * XST) = v3;
-            }
+            for (int k = 0; k < 4; k++)
+#pragma unroll
+                for (int rp = 0; rp < 2; rp++) {
+                    *reinterpret_cast<float*>(vb + ((2 * rp) * 4 + k) * XST) = v[k][rp].x;
+                    *reinterpret_cast<float*>(vb + ((2 * rp + 1) * 4 + k) * XST) = v[k][rp].y;
+                }
         }
     };
     const int co0 = w * 16 * NN + h * 4;
+    // (peeling the first chunk so that its MFMAs take C = 0 instead of this zeroing pass made the
+    // register allocation spill: 30 VGPRs at F = 256)
     f32x4 acc[16][NN];
 #pragma unroll
     for (int x = 0; x < 16; x++)
@@ -169,28 +196,21 @@ __device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
     // weight ring: fragment (16-channel group kc, point xi, co/16 = NN w + n) at ((kc 16 + xi) CF + co/16) KB
     const int voff = wino_voff<F>(w, lane);
     {
-        float d0[IT][4][4];
+        f32x2 d0[IT][4][2];
         tload(0, d0);
         tstore(0, d0);
     }
     __syncthreads();
     // B fragment of this wave's step t: 16-channel group t / 16 of the chunk, point t % 16
     auto boff = [](int t) { return (t / 16) * 1024 + (t % 16) * XST; };
-#ifdef AZ_WINO_NOBAR   // timing experiment only (wrong results): no chunk barrier, B read-ahead across chunks
-    f32x4 bq[LA];
-#pragma unroll
-    for (int i = 0; i < LA; i++) bq[i] = *reinterpret_cast<const f32x4*>(ldsb + vbase + vrd + boff(i));
-#endif
 #pragma unroll 1
     for (int c = 0; c < NCHUNK; c++) {
-        float dn[IT][4][4];
+        f32x2 dn[IT][4][2];
         const int vb = vbase + (c & 1) * VBYTES + vrd;
         const bool more = c + 1 < NCHUNK;
-#ifndef AZ_WINO_NOBAR
         f32x4 bq[LA];
 #pragma unroll
         for (int i = 0; i < LA; i++) bq[i] = *reinterpret_cast<const f32x4*>(ldsb + vb + boff(i));
-#endif
 #pragma unroll
         for (int st = 0; st < SPX; st++) {
             f32x4 B[XS];
@@ -199,9 +219,6 @@ __device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
                 const int t = st * XS + xs;
                 B[xs] = bq[t % LA];
                 if (t + LA < SPC) bq[t % LA] = *reinterpret_cast<const f32x4*>(ldsb + vb + boff(t + LA));
-#ifdef AZ_WINO_NOBAR
-                else if (more) bq[t % LA] = *reinterpret_cast<const f32x4*>(ldsb + vbase + ((c + 1) & 1) * VBYTES + vrd + boff(t + LA - SPC));
-#endif
             }
             f32x4 a[XS][NN];
 #pragma unroll
@@ -215,13 +232,15 @@ __device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
                 const bool nxt = cadd > 0 && !more;
                 const int tn = c * SPX + st + PF;
                 const int to = (nxt ? tn - NCHUNK * SPX : tn) * XS;
+                // the step's (wave-uniform) offset rides in the instruction's SGPR offset, the
+                // fragment's in the lane offset + immediate: no VALU address arithmetic per load
 #pragma unroll
                 for (int xs = 0; xs < XS; xs++)
 #pragma unroll
                     for (int n = 0; n < NN; n++)
                         wr[st % PF][xs][n] = __builtin_bit_cast(
-                            f32x4, __builtin_amdgcn_raw_buffer_load_b128(nxt ? rN : rW,
-                                                                         voff + n * 1024 + (to + xs) * CF * 1024, 0, 0));
+                            f32x4, __builtin_amdgcn_raw_buffer_load_b128(nxt ? rN : rW, voff + n * 1024,
+                                                                         (to + xs) * CF * 1024, 0));
             }
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -249,33 +268,33 @@ __device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
                 if (st == (TSG + WINO_TSPLIT) / XS && more && late) tstore((c + 1) & 1, dn);
             }
         }
-#ifndef AZ_WINO_NOBAR
         __syncthreads();
-#endif
     }
-#ifdef AZ_WINO_NOBAR
-    __syncthreads();
-#endif
-    // output transform Y = A^T M A per (output fragment n, channel r), + bias
+    // output transform Y = A^T M A per (output fragment n, channel pair), + bias: the two channels
+    // of a pair sit in consecutive accumulator registers, so every add is one v_pk_add_f32
 #pragma unroll
     for (int n = 0; n < NN; n++) {
-        const float4 bb = bias ? *reinterpret_cast<const float4*>(bias + co0 + n * 16) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const f32x4 bb = bias ? *reinterpret_cast<const f32x4*>(bias + co0 + n * 16) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
-            float m[4][4];
+        for (int p = 0; p < 2; p++) {
+            f32x2 m[16];
 #pragma unroll
-            for (int x = 0; x < 16; x++) m[x >> 2][x & 3] = acc[x][n][r];
-            float s0[4], s1[4];
+            for (int x = 0; x < 16; x++) m[x] = p ? f32x2{acc[x][n][2], acc[x][n][3]} : f32x2{acc[x][n][0], acc[x][n][1]};
+            const f32x2 br = p ? f32x2{bb[2], bb[3]} : f32x2{bb[0], bb[1]};
+            f32x2 s0[4], s1[4];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                s0[j] = m[0][j] + m[1][j] + m[2][j];
-                s1[j] = m[1][j] - m[2][j] - m[3][j];
+                s0[j] = pk_add(pk_add(m[j], m[4 + j]), m[8 + j]);
+                s1[j] = pk_sub(pk_sub(m[4 + j], m[8 + j]), m[12 + j]);
             }
-            const float br = r == 0 ? bb.x : r == 1 ? bb.y : r == 2 ? bb.z : bb.w;
-            y[n][0][r] = (s0[0] + s0[1] + s0[2]) + br;
-            y[n][1][r] = (s0[1] - s0[2] - s0[3]) + br;
-            y[n][2][r] = (s1[0] + s1[1] + s1[2]) + br;
-            y[n][3][r] = (s1[1] - s1[2] - s1[3]) + br;
+            const f32x2 q0 = pk_add(pk_add(pk_add(s0[0], s0[1]), s0[2]), br);
+            const f32x2 q1 = pk_add(pk_sub(pk_sub(s0[1], s0[2]), s0[3]), br);
+            const f32x2 q2 = pk_add(pk_add(pk_add(s1[0], s1[1]), s1[2]), br);
+            const f32x2 q3 = pk_add(pk_sub(pk_sub(s1[1], s1[2]), s1[3]), br);
+            y[n][0][2 * p] = q0.x; y[n][0][2 * p + 1] = q0.y;
+            y[n][1][2 * p] = q1.x; y[n][1][2 * p + 1] = q1.y;
+            y[n][2][2 * p] = q2.x; y[n][2][2 * p + 1] = q2.y;
+            y[n][3][2 * p] = q3.x; y[n][3][2 * p + 1] = q3.y;
         }
     }
 }

@@ -196,28 +196,41 @@ def test_c5_full_loop_20x256(require_gpu):
 
 def test_winograd_training_convs_match_direct(require_gpu, monkeypatch):
     """The 20x256 training step's residual convs (forward and data grad) as Winograd F(2x2,3x3)
-    (conv_wino_train_kernel, the inference tower's core) against the implicit-GEMM direct convs
-    (AZ_TRAIN_WINOGRAD=0) on the same batch: losses within 1e-5, every gradient tensor within 1e-4
-    relative norm (f32 rounding only; the oracle comparison above runs on the Winograd path)."""
-    blocks, filters, n = 20, 256, 8
+    (conv_wino_train_kernel, the inference tower's core) and as implicit-GEMM direct convs
+    (AZ_TRAIN_WINOGRAD=0) on the same batch, each against the float64 oracle following that path's
+    own ReLU masks: losses within 1e-5, every gradient tensor within 1e-4 relative norm.  The two
+    paths round differently, so a pre-activation within f32 rounding of 0 can take different ReLU
+    branches in them: path against path is held to the unmasked tolerance, 1e-2 (module docstring)."""
+    blocks, filters, n = 20, 256, 4
     w = A.random_weights(blocks, filters, seed=5)
     planes, tpol, tval = batch(n, seed=77)
+    seg, _ = T.segments(blocks, filters)
+    zero_bias = bn_fed_biases(blocks)
+    stats = ~T.trainable_mask(blocks, filters)
     out = {}
     for flag in ("1", "0"):
         monkeypatch.setenv("AZ_TRAIN_WINOGRAD", flag)
         tr = A.Trainer(blocks, filters, weights=w, max_batch=n)
-        out[flag] = (tr.compute_gradients(planes, tpol, tval), tr.grads(), tr.params())
-    (l1, g1, p1), (l0, g0, p0) = out["1"], out["0"]
-    assert abs(l1[0] - l0[0]) <= 1e-5 * (1 + abs(l0[0])) and abs(l1[1] - l0[1]) <= 1e-5 * (1 + abs(l0[1]))
-    seg, _ = T.segments(blocks, filters)
-    zero_bias = bn_fed_biases(blocks)
+        (pl, vl), g, p = tr.compute_gradients(planes, tpol, tval), tr.grads(), tr.params()
+        ref = T.TrainRef(blocks, filters, w)
+        rg, (rpl, rvl) = ref.grads(planes, tpol, tval, tr.relu_masks(n))
+        assert abs(pl - rpl) <= 1e-5 * (1 + abs(rpl)) and abs(vl - rvl) <= 1e-5 * (1 + abs(rvl)), (flag, pl, rpl, vl, rvl)
+        for name, (o, shape, bn) in seg.items():
+            size = int(np.prod(shape))
+            parts = [(name + ".gamma", o, shape[1]), (name + ".beta", o + shape[1], shape[1])] if bn else [(name, o, size)]
+            for pname, off, cnt in parts:
+                if pname in zero_bias:
+                    continue
+                a, r = g[off:off + cnt].astype(np.float64), rg[off:off + cnt]
+                err = np.linalg.norm(a - r) / max(np.linalg.norm(r), 1e-30)
+                assert err <= 1e-4, (flag, pname, err)
+        rs = ref.running_stats_flat(w)
+        assert np.all(np.abs(p[stats] - rs[stats]) <= 1e-5 * (1 + np.abs(rs[stats]))), flag
+        out[flag] = g
+    g1, g0 = out["1"].astype(np.float64), out["0"].astype(np.float64)
     for name, (o, shape, bn) in seg.items():
-        size = int(np.prod(shape))
-        parts = [(name + ".gamma", o, shape[1]), (name + ".beta", o + shape[1], shape[1])] if bn else [(name, o, size)]
-        for pname, off, cnt in parts:
-            if pname in zero_bias:
-                continue
-            a, r = g1[off:off + cnt].astype(np.float64), g0[off:off + cnt].astype(np.float64)
-            assert np.linalg.norm(a - r) <= 1e-4 * max(np.linalg.norm(r), 1e-30), pname
-    stats = ~T.trainable_mask(blocks, filters)
-    assert np.all(np.abs(p1[stats] - p0[stats]) <= 1e-5 * (1 + np.abs(p0[stats])))
+        if name in zero_bias:
+            continue
+        cnt = 2 * shape[1] if bn else int(np.prod(shape))
+        r = g0[o:o + cnt]
+        assert np.linalg.norm(g1[o:o + cnt] - r) <= 1e-2 * max(np.linalg.norm(r), 1e-30), name
