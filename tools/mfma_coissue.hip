@@ -1,7 +1,8 @@
 // mfma_coissue.hip -- how much VALU / LDS-read issue fits beside v_mfma_f32_16x16x4_f32 on gfx950
 // (design input for the f32 Winograd tower: DESIGN.md section 5.4).  Per wave: ITER iterations of
 // 8 independent MFMAs (8 accumulators) plus NV v_add_f32 (4 independent chains) and ND ds_read_b32
-// per iteration.  Grid: one workgroup per CU, WPS waves per SIMD.  Reports cycles per MFMA (the
+// per iteration.  AG: the accumulators in AccVGPRs (inline-asm MFMA with "+a") instead of ArchVGPRs
+// ("+v").  Grid: one workgroup per CU, WPS waves per SIMD.  Reports cycles per MFMA (the
 // issue floor is 32) from hipEvent time and the device clock (s_memtime delta per wave).
 // Build: hipcc --offload-arch=gfx950 -O3 -o tools/mfma_coissue tools/mfma_coissue.hip
 #include <hip/hip_runtime.h>
@@ -10,7 +11,7 @@
 
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 
-template <int NV, int ND>
+template <int NV, int ND, int AG>
 __global__ void __launch_bounds__(512) k(float* out, unsigned long long* cyc, int iters) {
     __shared__ float lds[4096];
     for (int i = threadIdx.x; i < 4096; i += blockDim.x) lds[i] = (float)i;
@@ -25,7 +26,9 @@ __global__ void __launch_bounds__(512) k(float* out, unsigned long long* cyc, in
     for (int it = 0; it < iters; it++) {
 #pragma unroll
         for (int m = 0; m < 8; m++) {
-            acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[m], 0, 0, 0);
+            if constexpr (AG == 1) asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+a"(acc[m]) : "v"(a), "v"(b));
+            else if constexpr (AG == 2) asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(acc[m]) : "v"(a), "v"(b));
+            else acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[m], 0, 0, 0);
 #pragma unroll
             for (int j = 0; j < NV / 8; j++) v[j & 3] = v[j & 3] + 1.0001f;
 #pragma unroll
@@ -40,15 +43,15 @@ __global__ void __launch_bounds__(512) k(float* out, unsigned long long* cyc, in
     if (lane == 0) cyc[blockIdx.x * 8 + (threadIdx.x >> 6)] = t1 - t0;
 }
 
-template <int NV, int ND>
+template <int NV, int ND, int AG = 0>
 void run(int wps, int iters, float* out, unsigned long long* cyc) {
     const int threads = 256 * wps, grid = 256;
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    k<NV, ND><<<grid, threads>>>(out, cyc, iters / 10);   // warm-up
+    k<NV, ND, AG><<<grid, threads>>>(out, cyc, iters / 10);   // warm-up
     hipEventRecord(e0);
-    k<NV, ND><<<grid, threads>>>(out, cyc, iters);
+    k<NV, ND, AG><<<grid, threads>>>(out, cyc, iters);
     hipEventRecord(e1);
     hipEventSynchronize(e1);
     float ms = 0;
@@ -61,8 +64,8 @@ void run(int wps, int iters, float* out, unsigned long long* cyc) {
         if (i % 8 < 4 * wps) { c += h[i]; n++; }
     c /= n;
     const double mfma_per_simd = 8.0 * iters * wps;
-    printf("waves/SIMD %d  VALU/MFMA %5.2f  DSread/MFMA %5.2f : %6.2f cycles per MFMA per SIMD (s_memtime), %.3f ms, "
-           "%.1f TFLOP/s\n", wps, NV / 8.0, ND / 8.0, c / mfma_per_simd, ms,
+    printf("%s  waves/SIMD %d  VALU/MFMA %5.2f  DSread/MFMA %5.2f : %6.2f cycles per MFMA per SIMD (s_memtime), %.3f ms, "
+           "%.1f TFLOP/s\n", AG == 1 ? "acc AGPR(asm)" : AG == 2 ? "acc VGPR(asm)" : "acc VGPR    ", wps, NV / 8.0, ND / 8.0, c / mfma_per_simd, ms,
            mfma_per_simd * 4 * 256 * 2048.0 / (ms * 1e-3) / 1e12);
     free(h);
 }
@@ -78,11 +81,16 @@ int main() {
         run<8, 0>(wps, iters, out, cyc);
         run<16, 0>(wps, iters, out, cyc);
         run<32, 0>(wps, iters, out, cyc);
-        run<48, 0>(wps, iters, out, cyc);
-        run<0, 8>(wps, iters, out, cyc);
-        run<0, 16>(wps, iters, out, cyc);
-        run<8, 8>(wps, iters, out, cyc);
-        run<16, 8>(wps, iters, out, cyc);
+        run<0, 0, 2>(wps, iters, out, cyc);
+        run<8, 0, 2>(wps, iters, out, cyc);
+        run<16, 0, 2>(wps, iters, out, cyc);
+        run<32, 0, 2>(wps, iters, out, cyc);
+        run<0, 0, 1>(wps, iters, out, cyc);
+        run<8, 0, 1>(wps, iters, out, cyc);
+        run<16, 0, 1>(wps, iters, out, cyc);
+        run<32, 0, 1>(wps, iters, out, cyc);
+        run<0, 8, 1>(wps, iters, out, cyc);
+        run<8, 8, 1>(wps, iters, out, cyc);
     }
     return 0;
 }
