@@ -155,14 +155,19 @@ conv_f32_kernel(const float* __restrict__ X, int ldx, int K, const float* __rest
 // partial[split][t][k][n]; reduced over splits in a fixed order by reduce_kernel.
 constexpr int GK = 64, GN = 64, GR = 64, GS = 80;
 
+// NB independent problems (X + i xbs, DY + i dbs: the 16 Winograd points of a weight grad) share
+// one launch: blockIdx.z = problem * splits + split, partial[split][problem][t][k][n].
 template <int TAPS>
 __global__ void __launch_bounds__(256)
 wgrad_f32_kernel(const float* __restrict__ X, int ldx, int K, const float* __restrict__ DY, int ldd, int N, int R,
-                 int rows_per_split, float* __restrict__ partial) {
+                 int rows_per_split, float* __restrict__ partial, int nb, size_t xbs, size_t dbs) {
     __shared__ __attribute__((aligned(16))) float xs[GR * GS + GS];
     __shared__ __attribute__((aligned(16))) float ds[GR * GS];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int k0 = blockIdx.x * GK, n0 = blockIdx.y * GN, split = blockIdx.z;
+    const int splits = gridDim.z / nb, split = blockIdx.z % splits, pb = blockIdx.z / splits;
+    const int k0 = blockIdx.x * GK, n0 = blockIdx.y * GN;
+    X += pb * xbs;
+    DY += pb * dbs;
     const int rbeg = split * rows_per_split, rend = min(R, rbeg + rows_per_split);
     f32x4 acc[TAPS][4];
 #pragma unroll
@@ -221,7 +226,7 @@ wgrad_f32_kernel(const float* __restrict__ X, int ldx, int K, const float* __res
 #pragma unroll
             for (int g = 0; g < 4; g++) {
                 const int kd = k0 + i * 16 + (lane >> 4) * 4 + g;
-                if (kd < K) partial[(((size_t)split * TAPS + t) * K + kd) * N + n] = acc[t][i][g];
+                if (kd < K) partial[((((size_t)split * nb + pb) * TAPS + t) * K + kd) * N + n] = acc[t][i][g];
             }
 }
 
@@ -556,6 +561,86 @@ __global__ void repack3x3_kernel(const float* __restrict__ w, int co_n, int ci_n
     }
 }
 
+// Winograd weight grad of a residual conv (F(2x2, 3x3), the forward conv's transforms
+// transposed): with V = B^T d B the input patch transform (as in the forward) and
+// M' = A dY A^T the 4x4 image of the tile's 2x2 output gradient (Y = A^T M A, so dL/dM = A dY A^T),
+//   dU[xi][ci][co] = sum over (board, tile) of V[xi][ci] M'[xi][co]   (16 GEMMs, wgrad_f32_kernel)
+//   dW[co][ci]     = G^T dU[co][ci] G                                   (U = G g G^T)
+// 2.25x fewer MFMAs than the 9-tap implicit GEMM.  Vt[xi][k][ci], Mt[xi][k][co] with
+// k = board * 16 + tile; one thread per (k, channel), channels fastest (coalesced).
+__global__ void __launch_bounds__(256) wino_wgrad_transform_kernel(const float* __restrict__ X,
+                                                                   const float* __restrict__ DY, int F, int B,
+                                                                   float* __restrict__ Vt, float* __restrict__ Mt) {
+    const size_t K = (size_t)B * 16, n = K * F;
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
+        const int c = (int)(e % F);
+        const size_t k = e / F;
+        const int t = (int)(k & 15), ty = t >> 2, tx = t & 3;
+        const size_t b64 = (k >> 4) * 64;
+        float d[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int r = 2 * ty - 1 + i, f = 2 * tx - 1 + j;
+                d[i][j] = ((unsigned)r < 8u && (unsigned)f < 8u) ? X[(b64 + r * 8 + f) * F + c] : 0.0f;
+            }
+        float y[2][2];
+#pragma unroll
+        for (int a = 0; a < 2; a++)
+#pragma unroll
+            for (int bb = 0; bb < 2; bb++) y[a][bb] = DY[(b64 + (2 * ty + a) * 8 + 2 * tx + bb) * F + c];
+        float tt[4][4], p[4][2];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            tt[0][j] = d[0][j] - d[2][j];
+            tt[1][j] = d[1][j] + d[2][j];
+            tt[2][j] = d[2][j] - d[1][j];
+            tt[3][j] = d[1][j] - d[3][j];
+        }
+#pragma unroll
+        for (int bb = 0; bb < 2; bb++) {
+            p[0][bb] = y[0][bb];
+            p[1][bb] = y[0][bb] + y[1][bb];
+            p[2][bb] = y[0][bb] - y[1][bb];
+            p[3][bb] = -y[1][bb];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const float v[4] = {tt[r][0] - tt[r][2], tt[r][1] + tt[r][2], tt[r][2] - tt[r][1], tt[r][1] - tt[r][3]};
+            const float m[4] = {p[r][0], p[r][0] + p[r][1], p[r][0] - p[r][1], -p[r][1]};
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                Vt[((size_t)(r * 4 + q) * K + k) * F + c] = v[q];
+                Mt[((size_t)(r * 4 + q) * K + k) * F + c] = m[q];
+            }
+        }
+    }
+}
+
+// dW = G^T dU G (f64, rounded once) into the gradient's burn layout g[co][ci][3][3]
+__global__ void __launch_bounds__(256) wino_wgrad_out_kernel(const float* __restrict__ dU, int F, float* __restrict__ g) {
+    const size_t n = (size_t)F * F;
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
+        const int co = (int)(e % F), ci = (int)(e / F);      // dU[xi][ci][co]
+        double u[4][4];
+#pragma unroll
+        for (int x = 0; x < 16; x++) u[x >> 2][x & 3] = dU[(size_t)x * n + e];
+        const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
+        double tg[3][4];
+#pragma unroll
+        for (int ky = 0; ky < 3; ky++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) tg[ky][j] = G[0][ky] * u[0][j] + G[1][ky] * u[1][j] + G[2][ky] * u[2][j] + G[3][ky] * u[3][j];
+#pragma unroll
+        for (int ky = 0; ky < 3; ky++)
+#pragma unroll
+            for (int kx = 0; kx < 3; kx++)
+                g[((size_t)co * F + ci) * 9 + ky * 3 + kx] =
+                    (float)(tg[ky][0] * G[0][kx] + tg[ky][1] * G[1][kx] + tg[ky][2] * G[2][kx] + tg[ky][3] * G[3][kx]);
+    }
+}
+
 // dWf[t][k][co] -> grad [co][ci][3][3]
 __global__ void unpack3x3_kernel(const float* __restrict__ dwf, int co_n, int ci_n, int kpad, float* __restrict__ g) {
     const size_t n = (size_t)co_n * ci_n * 9;
@@ -660,6 +745,7 @@ struct Trainer {
     bool wino = false;
     std::vector<float*> uf, ud;
     size_t ubytes = 0;
+    float *wvt = nullptr, *wmt = nullptr, *wdu = nullptr;   // Winograd weight-grad transforms, dU
     float *w40f = nullptr, *w40d = nullptr, *b40 = nullptr, *wp2f = nullptr, *w1d = nullptr;
     // saved activations (R = B*64 rows)
     float* x0 = nullptr;                     // [R][64] input planes
@@ -704,6 +790,7 @@ struct Trainer {
 namespace {
 
 constexpr int ROWS_PER_SPLIT = 512;   // weight-grad row split (8 boards)
+constexpr int WINO_ROWS_PER_SPLIT = 2048;   // Winograd weight grad: (board, tile) rows per split
 
 int launch_conv(Trainer* T, int taps, const float* X, int ldx, int K, const float* W, int N, const float* bias,
                 const float* addend, float* Y, int ldy, int R) {
@@ -741,11 +828,30 @@ int launch_wgrad(Trainer* T, int taps, const float* X, int ldx, int K, const flo
     const int rps = wgrad_rows_per_split(taps, R);
     const int splits = (int)wgrad_splits(taps, R);
     dim3 grid((K + tr::GK - 1) / tr::GK, (N + tr::GN - 1) / tr::GN, splits);
-    if (taps == 9) tr::wgrad_f32_kernel<9><<<grid, 256, 0, T->st>>>(X, ldx, K, DY, ldd, N, R, rps, T->wpart);
-    else tr::wgrad_f32_kernel<1><<<grid, 256, 0, T->st>>>(X, ldx, K, DY, ldd, N, R, rps, T->wpart);
+    if (taps == 9) tr::wgrad_f32_kernel<9><<<grid, 256, 0, T->st>>>(X, ldx, K, DY, ldd, N, R, rps, T->wpart, 1, 0, 0);
+    else tr::wgrad_f32_kernel<1><<<grid, 256, 0, T->st>>>(X, ldx, K, DY, ldd, N, R, rps, T->wpart, 1, 0, 0);
     const size_t n = (size_t)taps * K * N;
     tr::reduce_kernel<<<grid_for(n), 256, 0, T->st>>>(T->wpart, splits, n, out);
     return hipGetLastError() == hipSuccess ? 0 : fail("wgrad launch failed");
+}
+
+// Winograd weight grad of a residual F x F conv (input X, output gradient DY, B boards) into g
+int wino_rows_per_split(int B) { return B * 16 >= 8192 ? WINO_ROWS_PER_SPLIT : ROWS_PER_SPLIT; }
+size_t wino_splits(int B) { return (size_t)((B * 16 + wino_rows_per_split(B) - 1) / wino_rows_per_split(B)); }
+int launch_wino_wgrad(Trainer* T, const float* X, const float* DY, int B, float* g) {
+    const int F = T->F, K = B * 16;
+    if (B > T->Bmax) return fail("Winograd wgrad: batch too large");
+    if (wino_splits(B) * 16 * (size_t)F * F > T->wpart_cap) return fail("Winograd wgrad: partial buffer too small");
+    hipStream_t st = T->st;
+    tr::wino_wgrad_transform_kernel<<<grid_for((size_t)K * F), 256, 0, st>>>(X, DY, F, B, T->wvt, T->wmt);
+    const int rps = wino_rows_per_split(B), splits = (int)wino_splits(B);
+    dim3 grid(F / tr::GK, F / tr::GN, splits * 16);
+    tr::wgrad_f32_kernel<1><<<grid, 256, 0, st>>>(T->wvt, F, F, T->wmt, F, F, K, rps, T->wpart, 16, (size_t)K * F,
+                                                  (size_t)K * F);
+    const size_t n = (size_t)16 * F * F;
+    tr::reduce_kernel<<<grid_for(n), 256, 0, st>>>(T->wpart, splits, n, T->wdu);
+    tr::wino_wgrad_out_kernel<<<grid_for((size_t)F * F), 256, 0, st>>>(T->wdu, F, g);
+    return hipGetLastError() == hipSuccess ? 0 : fail("Winograd wgrad launch failed");
 }
 
 int nblk_rows(int R) { return (R + tr::CS_ROWS - 1) / tr::CS_ROWS; }
@@ -895,14 +1001,20 @@ int trainer_grads(Trainer* T, const float* planes, const float* tpol, const floa
         const auto& c2 = L.tower[2 + 2 * b];
         TRY(bn_backward(T, 2 + 2 * b, T->dx, T->xs[b + 1], T->y2[b], F, F, R, c2.bn, T->dy, T->dres));
         TRY(bias_grad(T, T->dy, F, F, R, T->g + c2.b));
-        TRY(launch_wgrad(T, 9, T->hh[b], F, F, T->dy, F, F, R, T->dwtmp, T->dwtmp_cap));
-        tr::unpack3x3_kernel<<<grid_for((size_t)9 * F * F), 256, 0, st>>>(T->dwtmp, F, F, F, T->g + c2.w);
+        if (T->wino) TRY(launch_wino_wgrad(T, T->hh[b], T->dy, B, T->g + c2.w));
+        else {
+            TRY(launch_wgrad(T, 9, T->hh[b], F, F, T->dy, F, F, R, T->dwtmp, T->dwtmp_cap));
+            tr::unpack3x3_kernel<<<grid_for((size_t)9 * F * F), 256, 0, st>>>(T->dwtmp, F, F, F, T->g + c2.w);
+        }
         if (T->wino) TRY(launch_wino(T, T->dy, T->ud[2 + 2 * b], nullptr, nullptr, T->dh, B));
         else TRY(launch_conv(T, 9, T->dy, F, F, T->wd[2 + 2 * b], F, nullptr, nullptr, T->dh, F, R));
         TRY(bn_backward(T, 1 + 2 * b, T->dh, T->hh[b], T->y1[b], F, F, R, c1.bn, T->dy, nullptr));
         TRY(bias_grad(T, T->dy, F, F, R, T->g + c1.b));
-        TRY(launch_wgrad(T, 9, T->xs[b], F, F, T->dy, F, F, R, T->dwtmp, T->dwtmp_cap));
-        tr::unpack3x3_kernel<<<grid_for((size_t)9 * F * F), 256, 0, st>>>(T->dwtmp, F, F, F, T->g + c1.w);
+        if (T->wino) TRY(launch_wino_wgrad(T, T->xs[b], T->dy, B, T->g + c1.w));
+        else {
+            TRY(launch_wgrad(T, 9, T->xs[b], F, F, T->dy, F, F, R, T->dwtmp, T->dwtmp_cap));
+            tr::unpack3x3_kernel<<<grid_for((size_t)9 * F * F), 256, 0, st>>>(T->dwtmp, F, F, F, T->g + c1.w);
+        }
         if (T->wino) TRY(launch_wino(T, T->dy, T->ud[1 + 2 * b], nullptr, T->dres, T->dxn, B));
         else TRY(launch_conv(T, 9, T->dy, F, F, T->wd[1 + 2 * b], F, nullptr, T->dres, T->dxn, F, R));
         std::swap(T->dx, T->dxn);
@@ -1034,6 +1146,12 @@ int az_trainer_create(int blocks, int filters, const float* weights, size_t n, i
     wp = std::max(wp, s1 * (size_t)F * 64);                             // heads 1x1
     wp = std::max(wp, s1 * 32 * 64);                                    // policy_conv_2
     wp = std::max(wp, sl * 512 * 64);                                   // value_linear_1
+    if (T->wino) {   // Winograd weight grads: [16][Bmax * 16][F] transforms, dU [16][F][F]
+        wp = std::max(wp, wino_splits(max_batch) * 16 * (size_t)F * F);
+        T->wvt = A((size_t)16 * max_batch * 16 * F);
+        T->wmt = A((size_t)16 * max_batch * 16 * F);
+        T->wdu = A((size_t)16 * F * F);
+    }
     T->wpart = A(wp);
     T->wpart_cap = wp;
     T->cpart = A((R / tr::CS_ROWS + 2) * 2 * (size_t)std::max(F, 65));

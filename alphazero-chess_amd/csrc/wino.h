@@ -132,21 +132,22 @@ __device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
     // V[buf] <- B^T d B of chunk c for this thread's item, in two halves: tload issues the patch
     // reads, tstore (WINO_TSPLIT steps later, their latency hidden behind MFMAs) transforms and writes.
     // d[it][j] = patch column j as row pairs {rows 0, 1}, {rows 2, 3} (one ds_read2st64_b32 each).
+    // element (i, j) of a patch is square (2 tty - 1 + i, 2 tl - 1 + j): rows off the board fall
+    // in the zero squares before / after ACT (WINO_PAD_SQ), so every row offset is an instruction
+    // immediate; the off-board columns (tl = 0: j = 0, tl = 3: j = 3) are read at a clamped
+    // on-board column (3 / 4: keeps the 32-lane groups of each read on distinct banks) and
+    // multiplied by 0 in tstore.  Column 1's lane offset, columns 0 / 3 relative to it.
+    constexpr int R16 = RS * 16, ROW = 8 * R16;
     auto tload = [&](int c, f32x2 (&d)[IT][4][2]) {
-        // patch addresses recomputed per chunk from a laundered index: hoisted out of the chunk
-        // loop they were loop-invariant registers, and spilled
+        // recomputed per chunk from a laundered index: one loop-invariant register more spilled
         const int tl = vgpr_index(ttx);
-        // element (i, j) of the patch is square (2 tty - 1 + i, 2 tl - 1 + j): rows off the board
-        // fall in the zero squares before / after ACT (WINO_PAD_SQ), so every row offset is an
-        // instruction immediate; the off-board columns (tl = 0: j = 0, tl = 3: j = 3) are read at a
-        // clamped on-board column (3 / 4: keeps the 32-lane groups of each read on distinct banks)
-        // and multiplied by 0 in tstore
-        constexpr int R16 = RS * 16, ROW = 8 * R16;
-        const int cs0 = tl > 0 ? 2 * tl - 1 : 3, cs3 = tl < 3 ? 2 * tl + 2 : 4;
+        const int pc1 = tl * (2 * R16) + (lane & 15) * 4;
+        const int pd0 = tl > 0 ? -R16 : 3 * R16, pd3 = tl < 3 ? 2 * R16 : -2 * R16;
 #pragma unroll
         for (int it = 0; it < IT; it++) {
-            const int base = (2 * tty - 1) * ROW + (c * CH + tchan(it)) * 4;
-            const int cb[4] = {base + cs0 * R16, base + 2 * tl * R16, base + (2 * tl + 1) * R16, base + cs3 * R16};
+            // tchan(it) - (lane & 15) is wave-uniform
+            const int b1 = pc1 + (2 * tty - 1) * ROW + (c * CH + tchan(it) - (lane & 15)) * 4;
+            const int cb[4] = {b1 + pd0, b1, b1 + R16, b1 + pd3};
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const char* p = ldsb + cb[j];
@@ -192,7 +193,16 @@ __device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
 #pragma unroll
     for (int x = 0; x < 16; x++)
 #pragma unroll
-        for (int n = 0; n < NN; n++) acc[x][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int n = 0; n < NN; n++) {
+            if constexpr (F == 256) {   // accumulators in VGPRs: 64-bit moves (the compiler's zeroing was 128 32-bit moves)
+                f32x2 z0, z1;
+                asm volatile("v_mov_b64 %0, 0" : "=v"(z0));
+                asm volatile("v_mov_b64 %0, 0" : "=v"(z1));
+                acc[x][n] = f32x4{z0.x, z0.y, z1.x, z1.y};
+            } else {                    // F = 64 keeps them in AGPRs, zeroed there directly
+                acc[x][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+        }
     // weight ring: fragment (16-channel group kc, point xi, co/16 = NN w + n) at ((kc 16 + xi) CF + co/16) KB
     const int voff = wino_voff<F>(w, lane);
     {
