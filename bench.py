@@ -33,7 +33,7 @@ PEAK_F32_TFLOPS = 157.3       # MI355X_MICROARCH.md: f32 MFMA = vector peak
 PEAK_HBM_GBS = 8000.0         # MI355X_MICROARCH.md: 8.0 TB/s spec
 # HBM bytes per tower launch from rocprofv3 PMC passes (tools/pmc_run.sh: FETCH_SIZE x2 per the
 # gfx950 correction + WRITE_SIZE), same kernel and per-launch work (2048 rows, 20x256)
-PMC_SUMMARY = {"f32": os.path.join(ROOT, "profiles", "r02_pmc_tower32w_s9_summary.json"),          # Winograd
+PMC_SUMMARY = {"f32": os.path.join(ROOT, "profiles", "r03_pmc_tower32w_5_summary.json"),           # Winograd
                "f32-direct": os.path.join(ROOT, "profiles", "r02_pmc_tower32_summary.json"),      # AZ_WINOGRAD=0
                "bf16": os.path.join(ROOT, "profiles", "r01_pmc_tower_v11_summary.json")}
 # mean plies of complete self-play games of this config (tools/game_length.py: 256 games, 20x256
@@ -145,18 +145,26 @@ def train_phase(args, A, rank, world, local):
     if rank != 0:
         return None
     flop = 3.0 * net_flop_per_eval(args.blocks, args.filters) * args.train_batch
+    # executed MFMA work: the residual convs of forward, data grad and weight grad run as Winograd
+    # F(2x2,3x3) at F = 256 (train.hip; AZ_TRAIN_WINOGRAD=0 restores direct convs)
+    wino = args.filters == 256 and os.environ.get("AZ_TRAIN_WINOGRAD", "1") != "0"
+    xflop = 3.0 * executed_flop_per_eval(args.blocks, args.filters, wino) * args.train_batch
     out = {"what": "training.rs:147-190 step: training-mode forward + backward + clip + AdamW, f32 "
                    "(v_mfma_f32_16x16x4_f32), %d positions per rank%s" %
                    (args.train_batch, ", gradients all-reduced over RCCL" if world > 1 else ""),
            "global_batch": args.train_batch * world, "dtype": "f32"}
     if res and ms == ms and ms != float("inf"):
-        tf = flop / (res["device_ms_per_step"] * 1e-3) / 1e12
+        tf = xflop / (res["device_ms_per_step"] * 1e-3) / 1e12
         out.update({"ms_per_step": ms, "samples_per_s": args.train_batch * world / (ms * 1e-3),
                     "device_ms_per_step": res["device_ms_per_step"],
                     "allreduce_ms_per_step": res["allreduce_ms_per_step"],
                     "allreduce_bytes": 4 * int(A._lib.lib.az_net_num_params(args.blocks, args.filters)),
                     "achieved_tflops": tf, "peak_tflops": PEAK_F32_TFLOPS, "frac": tf / PEAK_F32_TFLOPS,
-                    "flop_per_step": flop})
+                    "executed_flop_per_step": xflop, "residual_convs": "winograd" if wino else "direct",
+                    "algorithmic_flop_per_step": flop,
+                    "algorithmic_tflops": flop / (res["device_ms_per_step"] * 1e-3) / 1e12,
+                    "algorithmic_note": "3 x the direct-conv forward FLOPs (SURVEY 8a A6) / device time: "
+                                        "an equivalent rate, not a fraction of a peak"})
     else:
         out["error"] = err or "a rank failed"
     return out
@@ -165,6 +173,17 @@ def train_phase(args, A, rank, world, local):
 def net_flop_per_eval(B, F):
     """forward FLOPs per position"""
     return 2.0 * 64.0 * (171.0 * F + 18.0 * B * F * F + 40.0 * F + 2048.0) + 2.0 * (32768.0 + 64.0)
+
+
+def executed_flop_per_eval(B, F, winograd):
+    """The forward's FLOPs as the training kernels issue them: the 2B residual 3x3 convs as Winograd
+    F(2x2,3x3) (16 points x 16 tiles x F^2 multiply-adds per conv instead of 64 squares x 9 taps),
+    everything else direct"""
+    direct = net_flop_per_eval(B, F)
+    if not winograd:
+        return direct
+    resid = 2.0 * 64.0 * 18.0 * B * F * F
+    return direct - resid + 2.0 * (2 * B) * 256.0 * F * F
 
 
 def tower_algo_flop_per_row(B, F):
