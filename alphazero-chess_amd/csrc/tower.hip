@@ -808,12 +808,25 @@ tower32_kernel(const float* __restrict__ planes, TowerArgs ta, const int* __rest
 // The Winograd conv core is wino.h (shared with the training step).  conv_wino: one residual conv
 // of the tower, LDS -> LDS: the core, then + residual (the block input x, kept in the registers of
 // the wave that owns those outputs), ReLU, written back over the layer input in ACT.
+#ifdef AZ_TOWER_TRACE
+// trace build: per-wave phase stamps of the first AZ_TT_WG workgroups of the last launch
+// (slot layout in tools/tower_trace.py); read back with az_tower_trace_read
+constexpr int AZ_TT_WG = 8, AZ_TT_SLOTS = 2048;
+__device__ unsigned long long az_tower_trace_buf[AZ_TT_WG * 8 * AZ_TT_SLOTS];
+__device__ __forceinline__ unsigned long long* tt_slot(int w) {
+    return blockIdx.x < AZ_TT_WG && w < 8 ? az_tower_trace_buf + (blockIdx.x * 8 + w) * AZ_TT_SLOTS : nullptr;
+}
+#else
+__device__ __forceinline__ unsigned long long* tt_slot(int) { return nullptr; }
+#endif
+
 template <int F, bool RESID>
 __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase,
                                           const __amdgpu_buffer_rsrc_t rW, const __amdgpu_buffer_rsrc_t rN,
                                           const float* __restrict__ bias,
                                           f32x4 (&wr)[WinoCfg<F>::PF][WinoCfg<F>::XS][WinoCfg<F>::NN],
-                                          f32x4 (&xres)[WinoCfg<F>::NN][4], int w, int lane) {
+                                          f32x4 (&xres)[WinoCfg<F>::NN][4], int w, int lane,
+                                          unsigned long long* tr = nullptr) {
     constexpr int NN = WinoCfg<F>::NN, RS = F / 4 + 2;
     const int l16 = lane & 15, h = lane >> 4;
     const int ty = l16 >> 2, tx = l16 & 3;
@@ -827,7 +840,9 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase,
             for (int q = 0; q < 4; q++) xres[n][q] = *reinterpret_cast<const f32x4*>(ldsb + out_addr(n, q >> 1, q & 1));
     }
     f32x4 y[NN][4];
-    wino_core<F>(ldsb, vbase, rW, rN, bias, wr, w, lane, y);
+    wino_stamp(tr, 0);
+    wino_core<F>(ldsb, vbase, rW, rN, bias, wr, w, lane, y, tr);
+    wino_stamp(tr, 10);
 #pragma unroll
     for (int n = 0; n < NN; n++)
 #pragma unroll
@@ -838,6 +853,7 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase,
             for (int r = 0; r < 4; r++) v[r] = fmaxf(v[r], 0.0f);
             *reinterpret_cast<f32x4*>(ldsb + out_addr(n, q >> 1, q & 1)) = v;
         }
+    wino_stamp(tr, 11);
     __syncthreads();
 }
 
@@ -865,6 +881,11 @@ __device__ __forceinline__ void tower32w_board(const float* __restrict__ planes,
     const int zero_off = (XSZ + PAD + VSZ) * 16;
     static_assert((XSZ + PAD + VSZ) * 16 % 256 == 0, "conv32_lds ORs the zero row's offset into the low byte");
     char* ldsb = reinterpret_cast<char*>(X);
+    unsigned long long* tr = nullptr;
+#ifdef AZ_TOWER_TRACE
+    tr = tt_slot(w);
+#endif
+    wino_stamp(tr, 0);
     stage_planes_f32<1, RSI, NT>(V, planes, so, row0, 1, tid);
     for (int c = tid; c < ZN; c += NT) V[VSZ + c] = make_uint4(0, 0, 0, 0);
     for (int c = tid; c < PAD; c += NT) {
@@ -872,6 +893,7 @@ __device__ __forceinline__ void tower32w_board(const float* __restrict__ planes,
         X[XSZ + c] = make_uint4(0, 0, 0, 0);
     }
     __syncthreads();
+    wino_stamp(tr, 1);
     {   // input conv 19 (32) -> F: direct (18 k-steps)
         f32x4 wr[T32_PF][NN];
         const __amdgpu_buffer_rsrc_t r0 = t32_rsrc(ta.w[0], ta.wbytes[0]);
@@ -886,6 +908,7 @@ __device__ __forceinline__ void tower32w_board(const float* __restrict__ planes,
         conv32_lds<32, RSI, F, RSF, 1, NN, false>(ldsb, reinterpret_cast<char*>(X), vbase, zero_off, r0, rz, ta.b[0],
                                                   wr, w, 0, lane);
     }
+    wino_stamp(tr, 2);
     f32x4 xres[NN][4];
     f32x4 wring[PF][XS][NN];
     if (ta.blocks > 0) {
@@ -913,11 +936,12 @@ __device__ __forceinline__ void tower32w_board(const float* __restrict__ planes,
         const __amdgpu_buffer_rsrc_t r2 = t32_rsrc(ta.ww[2 * b + 1], ta.wwbytes[2 * b + 1]);
         const __amdgpu_buffer_rsrc_t r3 = t32_rsrc(b + 1 < ta.blocks ? ta.ww[2 * b + 2] : ta.ww[2 * b + 1], wb3);
 #endif
-        conv_wino<F, false>(ldsb, vbase, r1, r2, ta.b[1 + 2 * b], wring, xres, w, lane);
-        conv_wino<F, true>(ldsb, vbase, r2, r3, ta.b[2 + 2 * b], wring, xres, w, lane);
+        conv_wino<F, false>(ldsb, vbase, r1, r2, ta.b[1 + 2 * b], wring, xres, w, lane, tr ? tr + 3 + 64 * b : nullptr);
+        conv_wino<F, true>(ldsb, vbase, r2, r3, ta.b[2 + 2 * b], wring, xres, w, lane, tr ? tr + 35 + 64 * b : nullptr);
     }
     heads_group<F, RSF, 1, NT, SEARCH, true>(ldsb, reinterpret_cast<float*>(V), 0, 1, row0, tid, ta.head_frag32, ta.head,
                                              pol_out, val_out, so);
+    wino_stamp(tr, 3 + 64 * 20);
 }
 
 template <int F, bool SEARCH>
@@ -1093,3 +1117,13 @@ int tower_forward(NetDev* n, const void* planes, const int* count, int rows, flo
 }
 
 }  // namespace azi
+
+#ifdef AZ_TOWER_TRACE
+// trace build only: copy the phase stamps of the last tower launch (AZ_TT_WG x 8 waves x
+// AZ_TT_SLOTS u64) to the host
+extern "C" int az_tower_trace_read(unsigned long long* out, size_t n) {
+    const size_t cap = sizeof(azi::az_tower_trace_buf) / sizeof(unsigned long long);
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(azi::az_tower_trace_buf), (n < cap ? n : cap) * 8) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -37,6 +37,23 @@ AZ_PK3(pk_negx_sub_m3, "op_sel:[0,1,0] neg_lo:[0,0,1] neg_hi:[1,0,0]")      // (
 #undef AZ_PK2
 #undef AZ_PK3
 
+// Phase stamps for the tower trace build (make EXTRA=-DAZ_TOWER_TRACE, tools/tower_trace.c): shader
+// clock of one wave at a phase boundary, written by lane 0 through a vector store; `tr` is
+// nullptr (no code) in every other build
+__device__ __forceinline__ void wino_stamp(unsigned long long* tr, int k) {
+#ifdef AZ_TOWER_TRACE
+    if (tr) {
+        __builtin_amdgcn_sched_barrier(0);
+        unsigned long long t;
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+        __builtin_amdgcn_sched_barrier(0);
+        if ((threadIdx.x & 63) == 0) tr[k] = t;
+    }
+#else
+    (void)tr; (void)k;
+#endif
+}
+
 // zero squares before and after ACT ([64 squares][F/4 + 2 slots]): the transform reads the rows
 // above / below the board there
 constexpr int WINO_PAD_SQ = 8;
@@ -91,8 +108,10 @@ template <int F> __device__ __forceinline__ int wino_toff(int cg, int t) {
 // wino_core: one Winograd conv of the board whose layer input is in ACT ([64 squares][F/4 + 2
 // slots] f32 at ldsb, WINO_PAD_SQ zero squares on either side), V buffers at vbase: every wave's y[n][q] = this wave's outputs (output
 // fragment n, tile lane & 15, square (2 ty + q / 2, 2 tx + q % 2), channels co0 + 16 n + 0..3)
-// + bias (nullptr: none).  Ends after the last chunk's barrier: every wave has finished reading
-// ACT and V, so the caller may overwrite them.
+// + bias (nullptr: none).  Ends without a workgroup barrier: other waves may still be issuing
+// MFMAs on the last V buffer, but every read of ACT and of the other V buffer is done, so the caller
+// may overwrite ACT; it must pass a barrier before the next wino_core (which writes V) or before
+// reusing V.
 // wr: the weight ring; holds this conv's first PF steps on entry and the next conv's (rN) on
 // exit, so no layer starts on a cold weight fetch
 template <int F>
@@ -100,7 +119,8 @@ __device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
                                           const __amdgpu_buffer_rsrc_t rW, const __amdgpu_buffer_rsrc_t rN,
                                           const float* __restrict__ bias,
                                           f32x4 (&wr)[WinoCfg<F>::PF][WinoCfg<F>::XS][WinoCfg<F>::NN], int w,
-                                          int lane, f32x4 (&y)[WinoCfg<F>::NN][4]) {
+                                          int lane, f32x4 (&y)[WinoCfg<F>::NN][4],
+                                          unsigned long long* tr = nullptr) {
     constexpr int CF = F / 16, RS = F / 4 + 2;
     constexpr int NWV = WinoCfg<F>::NWV, NN = WinoCfg<F>::NN, XS = WinoCfg<F>::XS;
     constexpr int CH = WinoCfg<F>::CH, VBYTES = CH * 1024, XST = CH * 64;   // V buffer, xi stride
@@ -211,6 +231,7 @@ __device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
         tstore(0, d0);
     }
     __syncthreads();
+    wino_stamp(tr, 1);
     // B fragment of this wave's step t: 16-channel group t / 16 of the chunk, point t % 16
     auto boff = [](int t) { return (t / 16) * 1024 + (t % 16) * XST; };
 #pragma unroll 1
@@ -267,6 +288,7 @@ __device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
             // blocks at different steps, so that one of them keeps the matrix pipe busy (a stagger
             // that would not fit in this F's chunk is dropped)
             constexpr int TSG = (WINO_TSTAG + WINO_TSPLIT) / XS < SPX ? WINO_TSTAG : 0;
+            if (st == 4) wino_stamp(tr, 20 + c);
             if constexpr (TSG == 0) {
                 if (st == 0 && more) tload(c + 1, dn);
                 if (st == WINO_TSPLIT / XS && more) tstore((c + 1) & 1, dn);
@@ -278,7 +300,12 @@ __device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
                 if (st == (TSG + WINO_TSPLIT) / XS && more && late) tstore((c + 1) & 1, dn);
             }
         }
-        __syncthreads();
+        wino_stamp(tr, 12 + c);
+        // no barrier after the last chunk: the last transform reads of ACT and writes of V were
+        // ordered by the previous chunk's barrier, so the waves that finish first start their
+        // output transform beside the others' last MFMAs (C3 A/B: tower -0.6 %)
+        if (more) __syncthreads();
+        wino_stamp(tr, 2 + c);
     }
     // output transform Y = A^T M A per (output fragment n, channel pair), + bias: the two channels
     // of a pair sit in consecutive accumulator registers, so every add is one v_pk_add_f32
