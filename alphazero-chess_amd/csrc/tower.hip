@@ -825,14 +825,16 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase,
                                           const __amdgpu_buffer_rsrc_t rW, const __amdgpu_buffer_rsrc_t rN,
                                           const float* __restrict__ bias,
                                           f32x4 (&wr)[WinoCfg<F>::PF][WinoCfg<F>::XS][WinoCfg<F>::NN],
-                                          f32x4 (&xres)[WinoCfg<F>::NN][4], int w, int lane,
+                                          f32x4 (&xres)[WinoCfg<F>::NN][4], int w, int lane, bool pre_in,
+                                          bool pre_out, int* flag, int seq,
                                           unsigned long long* tr = nullptr) {
     constexpr int NN = WinoCfg<F>::NN, RS = F / 4 + 2;
     const int l16 = lane & 15, h = lane >> 4;
     const int ty = l16 >> 2, tx = l16 & 3;
     const int co0 = w * 16 * NN + h * 4;
     auto out_addr = [&](int n, int a, int b) { return ((2 * ty + a) * 8 + 2 * tx + b) * RS * 16 + (co0 + n * 16) * 4; };
-    // the residual: this wave's outputs of the block input, read before it is overwritten
+    // the residual: this wave's outputs of the block input, read before it is overwritten (kept in
+    // registers from the previous conv's epilogue instead: C3 A/B +0.4 %)
     if constexpr (!RESID) {
 #pragma unroll
         for (int n = 0; n < NN; n++)
@@ -841,7 +843,7 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase,
     }
     f32x4 y[NN][4];
     wino_stamp(tr, 0);
-    wino_core<F>(ldsb, vbase, rW, rN, bias, wr, w, lane, y, tr);
+    wino_core<F>(ldsb, vbase, rW, rN, bias, wr, w, lane, y, pre_in, tr);
     wino_stamp(tr, 10);
 #pragma unroll
     for (int n = 0; n < NN; n++)
@@ -854,6 +856,22 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase,
             *reinterpret_cast<f32x4*>(ldsb + out_addr(n, q >> 1, q & 1)) = v;
         }
     wino_stamp(tr, 11);
+    // F = 256: the next conv's chunk 0 is this conv's output channels 0-31, all written by wave 0;
+    // the first wave of each SIMD pair finishes ahead of its partner, so waves 0-3
+    // transform it into V[0] (free since the previous chunk barrier) while waves 4-7 finish, and the
+    // next conv starts on its MFMAs after this barrier.  Wave 0's stores are published to waves 1-3
+    // through an LDS flag (release / acquire at workgroup scope)
+    if constexpr (F == 256) {
+        if (pre_out && w < WinoCfg<F>::NWV / 2) {
+            if (w == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            else
+                while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != seq)
+                    __builtin_amdgcn_s_sleep(1);
+            WinoXf<F>(ldsb, vbase, w, lane).both(0, 0);
+        }
+    } else {
+        (void)pre_out; (void)flag; (void)seq;
+    }
     __syncthreads();
 }
 
@@ -872,7 +890,7 @@ __device__ __forceinline__ void tower32w_board(const float* __restrict__ planes,
     constexpr int PAD = WINO_PAD_SQ * RSF;               // zero squares either side of ACT
     static_assert(HeadsScratch<1, NT, heads_npart(NT, true)>::FLOATS * 4 <= VSZ * 16, "heads scratch must fit in V");
     static_assert(64 * RSI <= VSZ, "input planes must fit in V");
-    __shared__ __attribute__((aligned(16))) uint4 lds[PAD + XSZ + PAD + VSZ + ZN];
+    __shared__ __attribute__((aligned(16))) uint4 lds[PAD + XSZ + PAD + VSZ + ZN + 1];
     const int lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     uint4* X = lds + PAD;
@@ -887,7 +905,8 @@ __device__ __forceinline__ void tower32w_board(const float* __restrict__ planes,
 #endif
     wino_stamp(tr, 0);
     stage_planes_f32<1, RSI, NT>(V, planes, so, row0, 1, tid);
-    for (int c = tid; c < ZN; c += NT) V[VSZ + c] = make_uint4(0, 0, 0, 0);
+    for (int c = tid; c < ZN + 1; c += NT) V[VSZ + c] = make_uint4(0, 0, 0, 0);   // zero row + the pre-transform flag
+    int* flag = reinterpret_cast<int*>(V + VSZ + ZN);
     for (int c = tid; c < PAD; c += NT) {
         lds[c] = make_uint4(0, 0, 0, 0);
         X[XSZ + c] = make_uint4(0, 0, 0, 0);
@@ -936,8 +955,13 @@ __device__ __forceinline__ void tower32w_board(const float* __restrict__ planes,
         const __amdgpu_buffer_rsrc_t r2 = t32_rsrc(ta.ww[2 * b + 1], ta.wwbytes[2 * b + 1]);
         const __amdgpu_buffer_rsrc_t r3 = t32_rsrc(b + 1 < ta.blocks ? ta.ww[2 * b + 2] : ta.ww[2 * b + 1], wb3);
 #endif
-        conv_wino<F, false>(ldsb, vbase, r1, r2, ta.b[1 + 2 * b], wring, xres, w, lane, tr ? tr + 3 + 64 * b : nullptr);
-        conv_wino<F, true>(ldsb, vbase, r2, r3, ta.b[2 + 2 * b], wring, xres, w, lane, tr ? tr + 35 + 64 * b : nullptr);
+        // F = 256: each conv transforms the next conv's chunk 0 at its end (conv_wino; C3 A/B -0.3 %
+        // against the tail transform alone)
+        constexpr bool PRE = F == 256;
+        conv_wino<F, false>(ldsb, vbase, r1, r2, ta.b[1 + 2 * b], wring, xres, w, lane, PRE && b > 0, PRE, flag,
+                            2 * b + 1, tr ? tr + 3 + 64 * b : nullptr);
+        conv_wino<F, true>(ldsb, vbase, r2, r3, ta.b[2 + 2 * b], wring, xres, w, lane, PRE, PRE && b + 1 < ta.blocks,
+                           flag, 2 * b + 2, tr ? tr + 35 + 64 * b : nullptr);
     }
     heads_group<F, RSF, 1, NT, SEARCH, true>(ldsb, reinterpret_cast<float*>(V), 0, 1, row0, tid, ta.head_frag32, ta.head,
                                              pol_out, val_out, so);

@@ -105,60 +105,31 @@ template <int F> __device__ __forceinline__ int wino_toff(int cg, int t) {
     return ((cg * KPC + t / 16) * 16 + t % 16) * CF * 1024;
 }
 
-// wino_core: one Winograd conv of the board whose layer input is in ACT ([64 squares][F/4 + 2
-// slots] f32 at ldsb, WINO_PAD_SQ zero squares on either side), V buffers at vbase: every wave's y[n][q] = this wave's outputs (output
-// fragment n, tile lane & 15, square (2 ty + q / 2, 2 tx + q % 2), channels co0 + 16 n + 0..3)
-// + bias (nullptr: none).  Ends without a workgroup barrier: other waves may still be issuing
-// MFMAs on the last V buffer, but every read of ACT and of the other V buffer is done, so the caller
-// may overwrite ACT; it must pass a barrier before the next wino_core (which writes V) or before
-// reusing V.
-// wr: the weight ring; holds this conv's first PF steps on entry and the next conv's (rN) on
-// exit, so no layer starts on a cold weight fetch
-template <int F>
-__device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
-                                          const __amdgpu_buffer_rsrc_t rW, const __amdgpu_buffer_rsrc_t rN,
-                                          const float* __restrict__ bias,
-                                          f32x4 (&wr)[WinoCfg<F>::PF][WinoCfg<F>::XS][WinoCfg<F>::NN], int w,
-                                          int lane, f32x4 (&y)[WinoCfg<F>::NN][4],
-                                          unsigned long long* tr = nullptr) {
-    constexpr int CF = F / 16, RS = F / 4 + 2;
-    constexpr int NWV = WinoCfg<F>::NWV, NN = WinoCfg<F>::NN, XS = WinoCfg<F>::XS;
-    constexpr int CH = WinoCfg<F>::CH, VBYTES = CH * 1024, XST = CH * 64;   // V buffer, xi stride
-    constexpr int IT = CH * 16 / (NWV * 64);                       // transform items per thread per chunk
-    // t = (16-channel group kl, point t % 16) pairs of this wave per chunk; a ring step covers XS
-    constexpr int NCHUNK = F / CH, KPC = CH / 16, SPC = KPC * 16, SPX = SPC / XS;
-    constexpr int PF = WinoCfg<F>::PF, LA = WINO_LA * XS;
-    static_assert(NN * 16 * NWV == F && IT * NWV * 64 == CH * 16 && NWV % 4 == 0 && IT >= 1, "Winograd config");
-    static_assert(SPX % PF == 0 && SPC % LA == 0 && 16 % XS == 0, "ring slots must be compile-time");
-    const int l16 = lane & 15, h = lane >> 4;
-    // V[xi][quad cq][tile slot][4]: tile slot = tile ^ 2 (cq & 3).  gfx950 services a ds_read_b128
-    // in the lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31} (+32): each group holds quads h and
-    // h + 1 of a fragment at complementary tile sets, and the XOR by 2h keeps their 16 slots distinct
-    // (64 banks); a ds_write_b32 of the transform (32-lane groups, 32 banks) then covers 8 distinct
-    // slot values mod 8, so both are conflict-free (an XOR by 4h, laid out for groups of 16
-    // consecutive lanes, made every B-fragment read 2-way: PMC 48 % of LDS cycles were conflicts)
-    const int vrd = h * 256 + ((l16 ^ (2 * h)) * 16);               // + xi * XST + k * 1024 (cq = 4k + h, cq & 3 = h)
-    // transform items: wave w covers tile row ty = w & 3 and 16 channels per item: channel
-    // 16 (w >> 2 + it NWV / 4) + (lane & 15) of the chunk, tile (w & 3, lane >> 4) -- a patch read
-    // then touches 4 tiles of one row x 16 consecutive channels: conflict-free with the ACT row
-    // stride of 8 banks mod 64
-    const int tty = w & 3, ttx = lane >> 4;
-    auto tchan = [&](int it) { return 16 * ((w >> 2) + it * (NWV / 4)) + (lane & 15); };
-    auto vwr = [&](int tch) {   // + xi * XST
+// The input transform V[buf] <- B^T d B of one chunk, one (channel, tile) item per thread and
+// item slot.  Items: wave w covers tile row ty = w & 3 and 16 channels per item: channel
+// 16 (w >> 2 + g + it NWV / 4) + (lane & 15) of the chunk, tile (w & 3, lane >> 4) -- a patch read
+// then touches 4 tiles of one row x 16 consecutive channels: conflict-free with the ACT row stride
+// of 8 banks mod 64.  g = 1 names the item of the wave NWV / 4 waves later (used when one wave
+// transforms for two).  In two halves: load issues the patch reads, store transforms and writes V.
+// d[it][j] = patch column j as row pairs {rows 0, 1}, {rows 2, 3} (one ds_read2st64_b32 each).
+// Element (i, j) of a patch is square (2 ty - 1 + i, 2 tl - 1 + j): rows off the board fall in the
+// zero squares before / after ACT (WINO_PAD_SQ), so every row offset is an instruction immediate;
+// the off-board columns (tl = 0: j = 0, tl = 3: j = 3) are read at a clamped on-board column (3 / 4:
+// keeps the 32-lane groups of each read on distinct banks) and multiplied by 0 in store.
+template <int F> struct WinoXf {
+    static constexpr int NWV = WinoCfg<F>::NWV, CH = WinoCfg<F>::CH, RS = F / 4 + 2;
+    static constexpr int VBYTES = CH * 1024, XST = CH * 64, IT = CH * 16 / (NWV * 64);
+    static constexpr int R16 = RS * 16, ROW = 8 * R16;
+    typedef f32x2 Patch[IT][4][2];
+    char* ldsb;
+    int vbase, w, lane, tty, ttx;
+    __device__ __forceinline__ WinoXf(char* l, int vb, int w_, int lane_)
+        : ldsb(l), vbase(vb), w(w_), lane(lane_), tty(w_ & 3), ttx(lane_ >> 4) {}
+    __device__ __forceinline__ int tchan(int it, int g) const { return 16 * ((w >> 2) + g + it * (NWV / 4)) + (lane & 15); }
+    __device__ __forceinline__ int vwr(int tch) const {   // + xi * XST
         return (tch >> 2) * 256 + (((4 * tty + ttx) ^ (2 * ((tch >> 2) & 3))) * 16) + (tch & 3) * 4;
-    };
-    // V[buf] <- B^T d B of chunk c for this thread's item, in two halves: tload issues the patch
-    // reads, tstore (WINO_TSPLIT steps later, their latency hidden behind MFMAs) transforms and writes
-    // V[buf] <- B^T d B of chunk c for this thread's item, in two halves: tload issues the patch
-    // reads, tstore (WINO_TSPLIT steps later, their latency hidden behind MFMAs) transforms and writes.
-    // d[it][j] = patch column j as row pairs {rows 0, 1}, {rows 2, 3} (one ds_read2st64_b32 each).
-    // element (i, j) of a patch is square (2 tty - 1 + i, 2 tl - 1 + j): rows off the board fall
-    // in the zero squares before / after ACT (WINO_PAD_SQ), so every row offset is an instruction
-    // immediate; the off-board columns (tl = 0: j = 0, tl = 3: j = 3) are read at a clamped
-    // on-board column (3 / 4: keeps the 32-lane groups of each read on distinct banks) and
-    // multiplied by 0 in tstore.  Column 1's lane offset, columns 0 / 3 relative to it.
-    constexpr int R16 = RS * 16, ROW = 8 * R16;
-    auto tload = [&](int c, f32x2 (&d)[IT][4][2]) {
+    }
+    __device__ __forceinline__ void load(int c, Patch& d, int g = 0) const {
         // recomputed per chunk from a laundered index: one loop-invariant register more spilled
         const int tl = vgpr_index(ttx);
         const int pc1 = tl * (2 * R16) + (lane & 15) * 4;
@@ -166,7 +137,7 @@ __device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
 #pragma unroll
         for (int it = 0; it < IT; it++) {
             // tchan(it) - (lane & 15) is wave-uniform
-            const int b1 = pc1 + (2 * tty - 1) * ROW + (c * CH + tchan(it) - (lane & 15)) * 4;
+            const int b1 = pc1 + (2 * tty - 1) * ROW + (c * CH + tchan(it, g) - (lane & 15)) * 4;
             const int cb[4] = {b1 + pd0, b1, b1 + R16, b1 + pd3};
 #pragma unroll
             for (int j = 0; j < 4; j++) {
@@ -175,8 +146,8 @@ __device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
                 d[it][j][1] = f32x2{*reinterpret_cast<const float*>(p + 2 * ROW), *reinterpret_cast<const float*>(p + 3 * ROW)};
             }
         }
-    };
-    auto tstore = [&](int buf, const f32x2 (&d)[IT][4][2]) {
+    }
+    __device__ __forceinline__ void store(int buf, const Patch& d, int g = 0) const {
         const int tl = vgpr_index(ttx);
         // (m0, m3): 0 where patch column 0 / 3 is off the board
         const f32x2 m = f32x2{tl > 0 ? 1.0f : 0.0f, tl < 3 ? 1.0f : 0.0f};
@@ -195,7 +166,7 @@ __device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
             const f32x2 a2 = pk_sub(A[2], A[1]), a3 = pk_sub_m3(A[3], m, A[1]);
             const f32x2 b0 = pk_negx_fma_m0(B[0], m, B[2]), b1 = pk_negx_add(B[1], B[2]);
             const f32x2 b2 = pk_negx_sub(B[2], B[1]), b3 = pk_negx_sub_m3(B[3], m, B[1]);
-            char* vb = ldsb + vbase + buf * VBYTES + vwr(tchan(it));
+            char* vb = ldsb + vbase + buf * VBYTES + vwr(tchan(it, g));
             const f32x2 v[4][2] = {{a0, b0}, {a1, b1}, {a2, b2}, {a3, b3}};   // [column k][row pair]
 #pragma unroll
             for (int k = 0; k < 4; k++)
@@ -205,7 +176,53 @@ __device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
                     *reinterpret_cast<float*>(vb + ((2 * rp + 1) * 4 + k) * XST) = v[k][rp].y;
                 }
         }
-    };
+    }
+    // the first NWV / 2 waves transform chunk c into V[buf] for all NWV waves (their own items and
+    // those of the waves NWV / 2 later): F = 256 only (IT = 1, NWV = 8)
+    __device__ __forceinline__ void both(int c, int buf) const {
+        static_assert(IT == 1 && NWV == 8, "two items per thread of the first half");
+        Patch d0, d1;
+        load(c, d0, 0);
+        load(c, d1, 1);
+        store(buf, d0, 0);
+        store(buf, d1, 1);
+    }
+};
+
+// wino_core: one Winograd conv of the board whose layer input is in ACT ([64 squares][F/4 + 2
+// slots] f32 at ldsb, WINO_PAD_SQ zero squares on either side), V buffers at vbase: every wave's y[n][q] = this wave's outputs (output
+// fragment n, tile lane & 15, square (2 ty + q / 2, 2 tx + q % 2), channels co0 + 16 n + 0..3)
+// + bias (nullptr: none).  Ends without a workgroup barrier: other waves may still be issuing
+// MFMAs on the last V buffer, but every read of ACT and of the other V buffer is done, so the caller
+// may overwrite ACT; it must pass a barrier before the next wino_core (which writes V) or before
+// reusing V.
+// wr: the weight ring; holds this conv's first PF steps on entry and the next conv's (rN) on
+// exit, so no layer starts on a cold weight fetch
+template <int F>
+__device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
+                                          const __amdgpu_buffer_rsrc_t rW, const __amdgpu_buffer_rsrc_t rN,
+                                          const float* __restrict__ bias,
+                                          f32x4 (&wr)[WinoCfg<F>::PF][WinoCfg<F>::XS][WinoCfg<F>::NN], int w,
+                                          int lane, f32x4 (&y)[WinoCfg<F>::NN][4], bool pre = false,
+                                          unsigned long long* tr = nullptr) {
+    constexpr int CF = F / 16;
+    constexpr int NWV = WinoCfg<F>::NWV, NN = WinoCfg<F>::NN, XS = WinoCfg<F>::XS;
+    constexpr int CH = WinoCfg<F>::CH, VBYTES = CH * 1024, XST = CH * 64;   // V buffer, xi stride
+    constexpr int IT = CH * 16 / (NWV * 64);                       // transform items per thread per chunk
+    // t = (16-channel group kl, point t % 16) pairs of this wave per chunk; a ring step covers XS
+    constexpr int NCHUNK = F / CH, KPC = CH / 16, SPC = KPC * 16, SPX = SPC / XS;
+    constexpr int PF = WinoCfg<F>::PF, LA = WINO_LA * XS;
+    static_assert(NN * 16 * NWV == F && IT * NWV * 64 == CH * 16 && NWV % 4 == 0 && IT >= 1, "Winograd config");
+    static_assert(SPX % PF == 0 && SPC % LA == 0 && 16 % XS == 0, "ring slots must be compile-time");
+    const int l16 = lane & 15, h = lane >> 4;
+    // V[xi][quad cq][tile slot][4]: tile slot = tile ^ 2 (cq & 3).  gfx950 services a ds_read_b128
+    // in the lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31} (+32): each group holds quads h and
+    // h + 1 of a fragment at complementary tile sets, and the XOR by 2h keeps their 16 slots distinct
+    // (64 banks); a ds_write_b32 of the transform (32-lane groups, 32 banks) then covers 8 distinct
+    // slot values mod 8, so both are conflict-free (an XOR by 4h, laid out for groups of 16
+    // consecutive lanes, made every B-fragment read 2-way: PMC 48 % of LDS cycles were conflicts)
+    const int vrd = h * 256 + ((l16 ^ (2 * h)) * 16);               // + xi * XST + k * 1024 (cq = 4k + h, cq & 3 = h)
+    const WinoXf<F> xf(ldsb, vbase, w, lane);
     const int co0 = w * 16 * NN + h * 4;
     // (peeling the first chunk so that its MFMAs take C = 0 instead of this zeroing pass made the
     // register allocation spill: 30 VGPRs at F = 256)
@@ -225,12 +242,12 @@ __device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
         }
     // weight ring: fragment (16-channel group kc, point xi, co/16 = NN w + n) at ((kc 16 + xi) CF + co/16) KB
     const int voff = wino_voff<F>(w, lane);
-    {
+    if (!pre) {   // chunk 0 not transformed by the caller
         f32x2 d0[IT][4][2];
-        tload(0, d0);
-        tstore(0, d0);
+        xf.load(0, d0);
+        xf.store(0, d0);
+        __syncthreads();
     }
-    __syncthreads();
     wino_stamp(tr, 1);
     // B fragment of this wave's step t: 16-channel group t / 16 of the chunk, point t % 16
     auto boff = [](int t) { return (t / 16) * 1024 + (t % 16) * XST; };
@@ -284,20 +301,22 @@ __device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
                         acc[x][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[xs][n][s4], B[xs][s4], acc[x][n], 0, 0, 0);
                     }
             __builtin_amdgcn_sched_barrier(0);
-            // the next chunk's transform; the two waves of a SIMD pair run their transform VALU
-            // blocks at different steps, so that one of them keeps the matrix pipe busy (a stagger
-            // that would not fit in this F's chunk is dropped)
-            constexpr int TSG = (WINO_TSTAG + WINO_TSPLIT) / XS < SPX ? WINO_TSTAG : 0;
+            // the next chunk's transform.  F = 256: the first wave of each SIMD pair, which runs ahead
+            // of its partner by ~30 % of a chunk, transforms both waves' items after
+            // its last step, beside its partner's last MFMAs (C3 A/B: tower -1.1 % against one item
+            // per wave at staggered steps); other F: one item per wave, the two waves of a SIMD pair
+            // WINO_TSTAG steps apart (a stagger that would not fit in this F's chunk is dropped)
             if (st == 4) wino_stamp(tr, 20 + c);
-            if constexpr (TSG == 0) {
-                if (st == 0 && more) tload(c + 1, dn);
-                if (st == WINO_TSPLIT / XS && more) tstore((c + 1) & 1, dn);
+            if constexpr (F == 256) {
+                (void)dn;
+                if (st == SPX - 1 && more && w < NWV / 2) xf.both(c + 1, (c + 1) & 1);
             } else {
-                const bool late = w >= NWV / 2;
-                if (st == 0 && more && !late) tload(c + 1, dn);
-                if (st == TSG / XS && more && late) tload(c + 1, dn);
-                if (st == WINO_TSPLIT / XS && more && !late) tstore((c + 1) & 1, dn);
-                if (st == (TSG + WINO_TSPLIT) / XS && more && late) tstore((c + 1) & 1, dn);
+                constexpr int TSG = (WINO_TSTAG + WINO_TSPLIT) / XS < SPX ? WINO_TSTAG : 0;
+                const bool late = TSG > 0 && w >= NWV / 2;
+                if (st == 0 && more && !late) xf.load(c + 1, dn);
+                if (TSG > 0 && st == TSG / XS && more && late) xf.load(c + 1, dn);
+                if (st == WINO_TSPLIT / XS && more && !late) xf.store((c + 1) & 1, dn);
+                if (TSG > 0 && st == (TSG + WINO_TSPLIT) / XS && more && late) xf.store((c + 1) & 1, dn);
             }
         }
         wino_stamp(tr, 12 + c);
