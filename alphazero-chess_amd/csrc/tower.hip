@@ -826,15 +826,15 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase,
                                           const float* __restrict__ bias,
                                           f32x4 (&wr)[WinoCfg<F>::PF][WinoCfg<F>::XS][WinoCfg<F>::NN],
                                           f32x4 (&xres)[WinoCfg<F>::NN][4], int w, int lane, bool pre_in,
-                                          bool pre_out, int* flag, int seq,
+                                          bool pre_out, int vsel, int* flag, int seq,
                                           unsigned long long* tr = nullptr) {
-    constexpr int NN = WinoCfg<F>::NN, RS = F / 4 + 2;
+    constexpr int NN = WinoCfg<F>::NN, RS = F / 4 + 2, VBYTES = WinoCfg<F>::CH * 1024;
     const int l16 = lane & 15, h = lane >> 4;
     const int ty = l16 >> 2, tx = l16 & 3;
     const int co0 = w * 16 * NN + h * 4;
     auto out_addr = [&](int n, int a, int b) { return ((2 * ty + a) * 8 + 2 * tx + b) * RS * 16 + (co0 + n * 16) * 4; };
-    // the residual: this wave's outputs of the block input, read before it is overwritten (kept in
-    // registers from the previous conv's epilogue instead: C3 A/B +0.4 %)
+    // the residual: this wave's outputs of the block input, read before it is overwritten (keeping
+    // them in registers from the previous conv's epilogue instead measured +0.4 % at C3)
     if constexpr (!RESID) {
 #pragma unroll
         for (int n = 0; n < NN; n++)
@@ -843,8 +843,10 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase,
     }
     f32x4 y[NN][4];
     wino_stamp(tr, 0);
-    wino_core<F>(ldsb, vbase, rW, rN, bias, wr, w, lane, y, pre_in, tr);
+    // F = 64: the single chunk's V alternates between two buffers from conv to conv (vsel)
+    wino_core<F>(ldsb, vbase + (F == 64 ? vsel * VBYTES : 0), rW, rN, bias, wr, w, lane, y, pre_in, tr);
     wino_stamp(tr, 10);
+    f32x4 o[NN][4];
 #pragma unroll
     for (int n = 0; n < NN; n++)
 #pragma unroll
@@ -854,6 +856,7 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase,
 #pragma unroll
             for (int r = 0; r < 4; r++) v[r] = fmaxf(v[r], 0.0f);
             *reinterpret_cast<f32x4*>(ldsb + out_addr(n, q >> 1, q & 1)) = v;
+            o[n][q] = v;
         }
     wino_stamp(tr, 11);
     // F = 256: the next conv's chunk 0 is this conv's output channels 0-31, all written by wave 0;
@@ -869,9 +872,16 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase,
                     __builtin_amdgcn_s_sleep(1);
             WinoXf<F>(ldsb, vbase, w, lane).both(0, 0);
         }
+    } else if constexpr (F == 64) {
+        // F = 64: each wave's 16 output channels are a quarter of the next conv's single chunk;
+        // the wave transforms them from its registers (DPP neighbour exchange) into the other V
+        // buffer -- no ACT round trip, no barrier between the epilogue and the transform
+        (void)flag; (void)seq;
+        if (pre_out) wino_xform_regs<F>(o[0], ldsb + vbase + (1 - vsel) * VBYTES, w, lane);
     } else {
         (void)pre_out; (void)flag; (void)seq;
     }
+    (void)o;
     __syncthreads();
 }
 
@@ -884,7 +894,8 @@ __device__ __forceinline__ void tower32w_board(const float* __restrict__ planes,
     constexpr int RSF = F / 4 + 2, RSI = 32 / 4 + 2;
     constexpr int XSZ = 64 * RSF;                        // ACT, uint4 slots
     // both V buffers (one when a single chunk covers the input), also planes staging / heads scratch
-    constexpr int VSZ = (F / WinoCfg<F>::CH > 1 ? 2 : 1) * WinoCfg<F>::CH * 1024 / 16;
+    // (F = 64: two single-chunk buffers, alternating from conv to conv)
+    constexpr int VSZ = (F / WinoCfg<F>::CH > 1 || F == 64 ? 2 : 1) * WinoCfg<F>::CH * 1024 / 16;
     constexpr int PF = WinoCfg<F>::PF;
     constexpr int ZN = 16 + F / 4;
     constexpr int PAD = WINO_PAD_SQ * RSF;               // zero squares either side of ACT
@@ -955,13 +966,13 @@ __device__ __forceinline__ void tower32w_board(const float* __restrict__ planes,
         const __amdgpu_buffer_rsrc_t r2 = t32_rsrc(ta.ww[2 * b + 1], ta.wwbytes[2 * b + 1]);
         const __amdgpu_buffer_rsrc_t r3 = t32_rsrc(b + 1 < ta.blocks ? ta.ww[2 * b + 2] : ta.ww[2 * b + 1], wb3);
 #endif
-        // F = 256: each conv transforms the next conv's chunk 0 at its end (conv_wino; C3 A/B -0.3 %
-        // against the tail transform alone)
-        constexpr bool PRE = F == 256;
-        conv_wino<F, false>(ldsb, vbase, r1, r2, ta.b[1 + 2 * b], wring, xres, w, lane, PRE && b > 0, PRE, flag,
+        // F = 256 / 64: each conv transforms the next conv's chunk 0 at its end (conv_wino; C3 A/B
+        // -0.3 % against the tail transform alone)
+        constexpr bool PRE = F == 256 || F == 64;
+        conv_wino<F, false>(ldsb, vbase, r1, r2, ta.b[1 + 2 * b], wring, xres, w, lane, PRE && b > 0, PRE, 0, flag,
                             2 * b + 1, tr ? tr + 3 + 64 * b : nullptr);
         conv_wino<F, true>(ldsb, vbase, r2, r3, ta.b[2 + 2 * b], wring, xres, w, lane, PRE, PRE && b + 1 < ta.blocks,
-                           flag, 2 * b + 2, tr ? tr + 35 + 64 * b : nullptr);
+                           F == 64 ? 1 : 0, flag, 2 * b + 2, tr ? tr + 35 + 64 * b : nullptr);
     }
     heads_group<F, RSF, 1, NT, SEARCH, true>(ldsb, reinterpret_cast<float*>(V), 0, 1, row0, tid, ta.head_frag32, ta.head,
                                              pol_out, val_out, so);

@@ -147,27 +147,36 @@ template <int F> struct WinoXf {
             }
         }
     }
+    // B^T d B of one channel's patch: d[j] = column j as row pairs {rows 0, 1}, {rows 2, 3};
+    // v[k][rp] = (points (2 rp) 4 + k, (2 rp + 1) 4 + k); m = (m0, m3): 0 where patch column 0 / 3
+    // is off the board
+    static __device__ __forceinline__ void xform(const f32x2 (&d)[4][2], f32x2 m, f32x2 (&v)[4][2]) {
+        // rows: A[j] = (tt0, tt1) = (e0 - e2, e1 + e2), B[j] = (-tt2, tt3) = (e1 - e2, e1 - e3)
+        f32x2 A[4], B[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            A[j] = pk_rowa(d[j][0], d[j][1]);
+            B[j] = pk_rowb(d[j][0], d[j][1]);
+        }
+        // columns, two rows at a time: v0 = t0 m0 - t2, v1 = t1 + t2, v2 = t2 - t1, v3 = t1 - t3 m3
+        // (the same roundings as the scalar form: every multiply is by 1 or 0)
+        v[0][0] = pk_fma_m0_sub(A[0], m, A[2]);
+        v[1][0] = pk_add(A[1], A[2]);
+        v[2][0] = pk_sub(A[2], A[1]);
+        v[3][0] = pk_sub_m3(A[3], m, A[1]);
+        v[0][1] = pk_negx_fma_m0(B[0], m, B[2]);
+        v[1][1] = pk_negx_add(B[1], B[2]);
+        v[2][1] = pk_negx_sub(B[2], B[1]);
+        v[3][1] = pk_negx_sub_m3(B[3], m, B[1]);
+    }
     __device__ __forceinline__ void store(int buf, const Patch& d, int g = 0) const {
         const int tl = vgpr_index(ttx);
-        // (m0, m3): 0 where patch column 0 / 3 is off the board
         const f32x2 m = f32x2{tl > 0 ? 1.0f : 0.0f, tl < 3 ? 1.0f : 0.0f};
 #pragma unroll
         for (int it = 0; it < IT; it++) {
-            // rows: A[j] = (tt0, tt1) = (e0 - e2, e1 + e2), B[j] = (-tt2, tt3) = (e1 - e2, e1 - e3)
-            f32x2 A[4], B[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                A[j] = pk_rowa(d[it][j][0], d[it][j][1]);
-                B[j] = pk_rowb(d[it][j][0], d[it][j][1]);
-            }
-            // columns, two rows at a time: v0 = t0 m0 - t2, v1 = t1 + t2, v2 = t2 - t1, v3 = t1 - t3 m3
-            // (the same roundings as the scalar form: every multiply is by 1 or 0)
-            const f32x2 a0 = pk_fma_m0_sub(A[0], m, A[2]), a1 = pk_add(A[1], A[2]);
-            const f32x2 a2 = pk_sub(A[2], A[1]), a3 = pk_sub_m3(A[3], m, A[1]);
-            const f32x2 b0 = pk_negx_fma_m0(B[0], m, B[2]), b1 = pk_negx_add(B[1], B[2]);
-            const f32x2 b2 = pk_negx_sub(B[2], B[1]), b3 = pk_negx_sub_m3(B[3], m, B[1]);
+            f32x2 v[4][2];   // [column k][row pair]
+            xform(d[it], m, v);
             char* vb = ldsb + vbase + buf * VBYTES + vwr(tchan(it, g));
-            const f32x2 v[4][2] = {{a0, b0}, {a1, b1}, {a2, b2}, {a3, b3}};   // [column k][row pair]
 #pragma unroll
             for (int k = 0; k < 4; k++)
 #pragma unroll
@@ -188,6 +197,57 @@ template <int F> struct WinoXf {
         store(buf, d1, 1);
     }
 };
+
+// DPP row shift within the 16-lane rows: lane l reads lane l - N (SHR) / l + N (SHL); a source
+// outside the row reads 0 (bound_ctrl)
+template <int CTRL> __device__ __forceinline__ float row_dpp(float x) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
+}
+constexpr int DPP_SHL = 0x100, DPP_SHR = 0x110;
+
+// The next conv's input transform straight from a wave's conv outputs (F = 64: each wave's 16
+// output channels x all 16 tiles are one quarter of the single 64-channel chunk).  o[q] = the
+// lane's 4 channels (quad h of the wave's 16) at square (2 ty + q / 2, 2 tx + q % 2) of tile
+// l16 = 4 ty + tx.  A tile's 4x4 patch reaches one square into each neighbouring tile; the
+// neighbours' values come over DPP row shifts (tile +-1 = lane +-1, +-4 = lane +-4 within the
+// 16-lane row): off-board rows read 0 (outside the row), off-board columns read a finite value
+// that the transform multiplies by 0 -- exactly WinoXf::load + store on the same outputs in LDS,
+// bit for bit.  Writes the 16 points x 4 channels of the lane's (quad, tile) into V at vdst with
+// one ds_write_b128 per point.
+template <int F>
+__device__ __forceinline__ void wino_xform_regs(const f32x4 (&o)[4], char* __restrict__ vdst, int w, int lane) {
+    static_assert(F == 64 && WinoCfg<F>::NN == 1, "one chunk, one output fragment per wave");
+    constexpr int XST = WinoCfg<F>::CH * 64;
+    const int l16 = lane & 15, h = lane >> 4, tx = l16 & 3;
+    const int cq = w * 4 + h;                                       // channel quad of the chunk
+    const f32x2 m = f32x2{tx > 0 ? 1.0f : 0.0f, tx < 3 ? 1.0f : 0.0f};
+    f32x4 out[16];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const float q0 = o[0][r], q1 = o[1][r], q2 = o[2][r], q3 = o[3][r];
+        f32x2 d[4][2];
+        d[0][0] = f32x2{row_dpp<DPP_SHR + 5>(q3), row_dpp<DPP_SHR + 1>(q1)};
+        d[0][1] = f32x2{row_dpp<DPP_SHR + 1>(q3), row_dpp<DPP_SHL + 3>(q1)};
+        d[1][0] = f32x2{row_dpp<DPP_SHR + 4>(q2), q0};
+        d[1][1] = f32x2{q2, row_dpp<DPP_SHL + 4>(q0)};
+        d[2][0] = f32x2{row_dpp<DPP_SHR + 4>(q3), q1};
+        d[2][1] = f32x2{q3, row_dpp<DPP_SHL + 4>(q1)};
+        d[3][0] = f32x2{row_dpp<DPP_SHR + 3>(q2), row_dpp<DPP_SHL + 1>(q0)};
+        d[3][1] = f32x2{row_dpp<DPP_SHL + 1>(q2), row_dpp<DPP_SHL + 5>(q0)};
+        f32x2 v[4][2];
+        WinoXf<F>::xform(d, m, v);
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+#pragma unroll
+            for (int rp = 0; rp < 2; rp++) {
+                out[(2 * rp) * 4 + k][r] = v[k][rp].x;
+                out[(2 * rp + 1) * 4 + k][r] = v[k][rp].y;
+            }
+    }
+    char* vb = vdst + cq * 256 + ((l16 ^ (2 * (cq & 3))) * 16);
+#pragma unroll
+    for (int p = 0; p < 16; p++) *reinterpret_cast<f32x4*>(vb + p * XST) = out[p];
+}
 
 // wino_core: one Winograd conv of the board whose layer input is in ACT ([64 squares][F/4 + 2
 // slots] f32 at ldsb, WINO_PAD_SQ zero squares on either side), V buffers at vbase: every wave's y[n][q] = this wave's outputs (output

@@ -15,7 +15,7 @@ wgok = (t[:, :, 0] > 0).all(1)
 t = t[wgok]                                           # [wg, waves, NS]
 print("traced workgroups: %d" % t.shape[0])
 conv = np.stack([t[:, :, 3 + 32 * i: 35 + 32 * i] for i in range(2 * B)], 2)   # [wg, waves, convs, 32]
-end = 3 + 64 * B
+end = 3 + 64 * 20
 total = t[:, :, end] - t[:, :, 0]
 print("total %.0f cycles per board; staging %.0f, input conv %.0f, heads %.0f"
       % (total.mean(), (t[:, :, 1] - t[:, :, 0]).mean(), (t[:, :, 2] - t[:, :, 1]).mean(),
