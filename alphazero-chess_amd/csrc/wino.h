@@ -34,8 +34,6 @@ AZ_PK3(pk_fma_m0_sub, "op_sel_hi:[1,0,1] neg_lo:[0,0,1] neg_hi:[0,0,1]")    // (
 AZ_PK3(pk_sub_m3, "op_sel:[0,1,0] neg_lo:[1,0,0] neg_hi:[1,0,0]")          // (b.x - a.x m.y, b.y - a.y m.y)
 AZ_PK3(pk_negx_fma_m0, "op_sel_hi:[1,0,1] neg_lo:[1,0,0] neg_hi:[0,0,1]")   // (-a.x m.x + b.x, a.y m.x - b.y)
 AZ_PK3(pk_negx_sub_m3, "op_sel:[0,1,0] neg_lo:[0,0,1] neg_hi:[1,0,0]")      // (a.x m.y - b.x, -a.y m.y + b.y)
-#undef AZ_PK2
-#undef AZ_PK3
 
 // Phase stamps for the tower trace build (make EXTRA=-DAZ_TOWER_TRACE, tools/tower_trace.c): shader
 // clock of one wave at a phase boundary, written by lane 0 through a vector store; `tr` is
@@ -214,34 +212,71 @@ constexpr int DPP_SHL = 0x100, DPP_SHR = 0x110;
 // that the transform multiplies by 0 -- exactly WinoXf::load + store on the same outputs in LDS,
 // bit for bit.  Writes the 16 points x 4 channels of the lane's (quad, tile) into V at vdst with
 // one ds_write_b128 per point.
+AZ_PK2(pkc_nadd, "neg_lo:[1,1] neg_hi:[1,1]")                 // (-a.x - b.x, -a.y - b.y)
+AZ_PK3(pkc_fma_nc, "neg_lo:[0,0,1] neg_hi:[0,0,1]")            // (a.x m.x - c.x, a.y m.y - c.y)
+AZ_PK3(pkc_nfma, "neg_lo:[1,0,0] neg_hi:[1,0,0]")              // (-a.x m.x + c.x, -a.y m.y + c.y)
+#undef AZ_PK2
+#undef AZ_PK3
 template <int F>
 __device__ __forceinline__ void wino_xform_regs(const f32x4 (&o)[4], char* __restrict__ vdst, int w, int lane) {
     static_assert(F == 64 && WinoCfg<F>::NN == 1, "one chunk, one output fragment per wave");
     constexpr int XST = WinoCfg<F>::CH * 64;
     const int l16 = lane & 15, h = lane >> 4, tx = l16 & 3;
     const int cq = w * 4 + h;                                       // channel quad of the chunk
-    const f32x2 m = f32x2{tx > 0 ? 1.0f : 0.0f, tx < 3 ? 1.0f : 0.0f};
+    const float m0 = tx > 0 ? 1.0f : 0.0f, m3 = tx < 3 ? 1.0f : 0.0f;
+    const f32x2 m0v = f32x2{m0, m0}, m3v = f32x2{m3, m3};
     f32x4 out[16];
 #pragma unroll
-    for (int r = 0; r < 4; r++) {
-        const float q0 = o[0][r], q1 = o[1][r], q2 = o[2][r], q3 = o[3][r];
-        f32x2 d[4][2];
-        d[0][0] = f32x2{row_dpp<DPP_SHR + 5>(q3), row_dpp<DPP_SHR + 1>(q1)};
-        d[0][1] = f32x2{row_dpp<DPP_SHR + 1>(q3), row_dpp<DPP_SHL + 3>(q1)};
-        d[1][0] = f32x2{row_dpp<DPP_SHR + 4>(q2), q0};
-        d[1][1] = f32x2{q2, row_dpp<DPP_SHL + 4>(q0)};
-        d[2][0] = f32x2{row_dpp<DPP_SHR + 4>(q3), q1};
-        d[2][1] = f32x2{q3, row_dpp<DPP_SHL + 4>(q1)};
-        d[3][0] = f32x2{row_dpp<DPP_SHR + 3>(q2), row_dpp<DPP_SHL + 1>(q0)};
-        d[3][1] = f32x2{row_dpp<DPP_SHL + 1>(q2), row_dpp<DPP_SHL + 5>(q0)};
-        f32x2 v[4][2];
-        WinoXf<F>::xform(d, m, v);
+    for (int cp = 0; cp < 2; cp++) {   // channel pairs (2 cp, 2 cp + 1), packed in one f32x2
+        auto own = [&](int q) { return cp ? f32x2{o[q][2], o[q][3]} : f32x2{o[q][0], o[q][1]}; };
+        auto nb = [&](auto dpp, int q) { const f32x2 v = own(q); return f32x2{dpp(v.x), dpp(v.y)}; };
+        auto shr1 = [](float x) { return row_dpp<DPP_SHR + 1>(x); };
+        auto shr3 = [](float x) { return row_dpp<DPP_SHR + 3>(x); };
+        auto shr4 = [](float x) { return row_dpp<DPP_SHR + 4>(x); };
+        auto shr5 = [](float x) { return row_dpp<DPP_SHR + 5>(x); };
+        auto shl1 = [](float x) { return row_dpp<DPP_SHL + 1>(x); };
+        auto shl3 = [](float x) { return row_dpp<DPP_SHL + 3>(x); };
+        auto shl4 = [](float x) { return row_dpp<DPP_SHL + 4>(x); };
+        auto shl5 = [](float x) { return row_dpp<DPP_SHL + 5>(x); };
+        // P[i][j]: patch rows i (square row 2 ty - 1 + i), columns j
+        const f32x2 P[4][4] = {
+            {nb(shr5, 3), nb(shr4, 2), nb(shr4, 3), nb(shr3, 2)},
+            {nb(shr1, 1), own(0), own(1), nb(shl1, 0)},
+            {nb(shr1, 3), own(2), own(3), nb(shl1, 2)},
+            {nb(shl3, 1), nb(shl4, 0), nb(shl4, 1), nb(shl5, 0)}};
+        // rows (as WinoXf::xform): R0 = P0 - P2, R1 = P1 + P2, nR2 = P1 - P2, R3 = P1 - P3
+        f32x2 R[4][4];
 #pragma unroll
-        for (int k = 0; k < 4; k++)
+        for (int j = 0; j < 4; j++) {
+            R[0][j] = pk_sub(P[0][j], P[2][j]);
+            R[1][j] = pk_add(P[1][j], P[2][j]);
+            R[2][j] = pk_sub(P[1][j], P[2][j]);
+            R[3][j] = pk_sub(P[1][j], P[3][j]);
+        }
+        // columns: the operations of WinoXf::xform per point, two channels per instruction
+        f32x2 V[4][4];
+        V[0][0] = pkc_fma_nc(R[0][0], m0v, R[0][2]);
+        V[0][1] = pk_add(R[0][1], R[0][2]);
+        V[0][2] = pk_sub(R[0][2], R[0][1]);
+        V[0][3] = pkc_nfma(R[0][3], m3v, R[0][1]);
+        V[1][0] = pkc_fma_nc(R[1][0], m0v, R[1][2]);
+        V[1][1] = pk_add(R[1][1], R[1][2]);
+        V[1][2] = pk_sub(R[1][2], R[1][1]);
+        V[1][3] = pkc_nfma(R[1][3], m3v, R[1][1]);
+        V[2][0] = pkc_nfma(R[2][0], m0v, R[2][2]);
+        V[2][1] = pkc_nadd(R[2][1], R[2][2]);
+        V[2][2] = pk_sub(R[2][1], R[2][2]);
+        V[2][3] = pkc_fma_nc(R[2][3], m3v, R[2][1]);
+        V[3][0] = pkc_fma_nc(R[3][0], m0v, R[3][2]);
+        V[3][1] = pk_add(R[3][1], R[3][2]);
+        V[3][2] = pk_sub(R[3][2], R[3][1]);
+        V[3][3] = pkc_nfma(R[3][3], m3v, R[3][1]);
 #pragma unroll
-            for (int rp = 0; rp < 2; rp++) {
-                out[(2 * rp) * 4 + k][r] = v[k][rp].x;
-                out[(2 * rp + 1) * 4 + k][r] = v[k][rp].y;
+        for (int a = 0; a < 4; a++)
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                out[4 * a + b][2 * cp] = V[a][b].x;
+                out[4 * a + b][2 * cp + 1] = V[a][b].y;
             }
     }
     char* vb = vdst + cq * 256 + ((l16 ^ (2 * (cq & 3))) * 16);

@@ -36,6 +36,8 @@ PEAK_HBM_GBS = 8000.0         # MI355X_MICROARCH.md: 8.0 TB/s spec
 PMC_SUMMARY = {"f32": os.path.join(ROOT, "profiles", "r03_pmc_tower32w_5_summary.json"),           # Winograd
                "f32-direct": os.path.join(ROOT, "profiles", "r02_pmc_tower32_summary.json"),      # AZ_WINOGRAD=0
                "bf16": os.path.join(ROOT, "profiles", "r01_pmc_tower_v11_summary.json")}
+# simulation steps of the instrumented profile pass after the timed window (8 sampled tower launches)
+PROFILE_SIMS = 256
 # mean plies of complete self-play games of this config (tools/game_length.py: 256 games, 20x256
 # random-init seed 42, 800 sims/move, noise + temperature moves, played to the end)
 # (f32 Winograd net, the headline's; the round-1 file used the bf16 net and is only a fallback)
@@ -429,7 +431,9 @@ def main():
         synchronize()
 
     def phase(net, cache, steps, timing):
-        """Self-play from startpos: warmup steps, then `steps` timed steps of K simulation steps."""
+        """Self-play from startpos: warmup steps, then `steps` timed steps of K simulation steps; with
+        `timing`, every 32nd simulation step carries HIP events (roofline / tree_walk), in the window
+        or in a profile pass after it (persistent kernel)."""
         if args.rehearse:
             sp = RehearsalSelfPlay(G, S, sh["seed"])
         else:
@@ -440,7 +444,14 @@ def main():
             sp.run_sims(K)
             sp.drain()
         st0 = sp.search.stats()
-        sp.search.timing(reset=True, enable=timing)
+        # the sampled steps (every 32nd) run as separate kernels bracketed by events: inside the
+        # window when the engine steps with k_step + the tower (the events cost nothing measurable
+        # there, and the roofline then times launches of the window itself); with the persistent
+        # per-game kernel (C2) they would break it every 32 steps, so they go to a profile pass of
+        # PROFILE_SIMS steps after the window
+        persistent = bool(getattr(sp.search, "persistent", False))
+        inwin = timing and not persistent
+        sp.search.timing(reset=True, enable=inwin)
         barrier()
         t0 = time.perf_counter()
         finished = 0
@@ -451,20 +462,27 @@ def main():
         synchronize()
         barrier()
         elapsed = time.perf_counter() - t0
-        tm = sp.search.timing(reset=False, enable=False)
-        tm["persistent"] = bool(getattr(sp.search, "persistent", False))
         st1 = sp.search.stats()
-        c = [st1[k] - st0[k] for k in ("sims", "evals", "terminal_leaves", "moves", "max_depth_sum", "cache_hits")]
-        assert c[0] == G * K * steps, (c[0], G * K * steps)
-        elapsed, tot = reduce_run(elapsed, c + [finished], world)
         digests = None
         if world > 1 and not args.rehearse:
-            # per-rank fingerprint of the games (the current roots' visit arrays): distinct seeds
-            # must give distinct games on every rank
+            # per-rank fingerprint of the games (the roots' visit arrays at the end of the window):
+            # distinct seeds must give distinct games on every rank
             import hashlib
             _, vis, dep = sp.search.read_roots()
             digests = [None] * world
             dist.all_gather_object(digests, hashlib.sha1(vis.tobytes() + dep.tobytes()).hexdigest()[:16])
+        prof = min(PROFILE_SIMS, S) if timing and not inwin else 0
+        if prof:
+            sp.search.timing(reset=True, enable=True)
+            sp.run_sims(prof)
+            sp.drain()
+            synchronize()
+        tm = sp.search.timing(reset=False, enable=False)
+        tm["persistent"] = persistent
+        tm["profile_sim_steps"] = prof if prof else steps * K
+        c = [st1[k] - st0[k] for k in ("sims", "evals", "terminal_leaves", "moves", "max_depth_sum", "cache_hits")]
+        assert c[0] == G * K * steps, (c[0], G * K * steps)
+        elapsed, tot = reduce_run(elapsed, c + [finished], world)
         del sp
         res = dict(zip(("sims", "evals", "terminal", "moves", "depth", "hits", "finished"), tot))
         res["rank_root_digests"] = digests
@@ -501,9 +519,11 @@ def main():
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "traffic_ratio": (traffic / algo_bytes) if traffic else None,
                 "kernel": "%s: input conv + %d residual convs + heads in one launch, %s; %d launches timed (HIP events "
-                          "on every 32nd simulation step)"
+                          "on every 32nd simulation step %s)"
                           % (kname, 2 * B, "v_mfma_f32_16x16x32_bf16" if dtype == "bf16" else "v_mfma_f32_16x16x4_f32",
-                             tm["conv_launches"]),
+                             tm["conv_launches"],
+                             ("of a %d-step profile pass after the timed window" % tm["profile_sim_steps"])
+                             if tm["persistent"] else "of the timed window"),
                 "executed_flop_per_row": exec_row,
                 "executed_note": ("Winograd F(2x2,3x3): the residual convs execute 1/2.25 of the direct-conv "
                                   "multiplies; input conv (19 -> 32 padded channels) and the heads' MFMAs included"
@@ -564,9 +584,9 @@ def main():
     value = sims_all / elapsed
     tower_tflops = tm["tower_flop"] / (tm["tower_ms"] * 1e-3) / 1e12 if tm["tower_ms"] > 0 else 0.0
     peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
-    # select_bytes covers every k_select launch of the window (steps x K); the event times cover
-    # the sampled launches (az_timing: every 32nd simulation step)
-    sel_bytes_per_launch = tm["select_bytes"] / max(args.steps * K, 1)
+    # select_bytes covers every select walk of the timed window (or of the profile pass); the event
+    # times cover its sampled launches (az_timing: every 32nd simulation step)
+    sel_bytes_per_launch = tm["select_bytes"] / max(tm["profile_sim_steps"], 1)
     sel_ms_per_launch = tm["select_ms"] / max(tm["select_launches"], 1)
     sel_gbs = sel_bytes_per_launch / (sel_ms_per_launch * 1e-3) / 1e9 if tm["select_ms"] > 0 else 0.0
     out = {
@@ -609,10 +629,11 @@ def main():
                       "avg_ms_per_launch": tm["select_ms"] / max(tm["select_launches"], 1)},
         "sim_step_ms": {k: tm[k + "_ms"] / max(tm["sim_steps"], 1)
                         for k in ("select", "expand", "encode", "tower", "heads", "backup")},
-        "sim_kernels": ("k_sims32w<%d> for the untimed simulation steps: one workgroup per game runs its backup, "
-                        "select, expand and network evaluation with no grid-wide step boundary (the timed "
-                        "every-32nd steps, which carry the roofline / tree_walk events, run as separate kernels)"
-                        % args.filters) if tm.get("persistent") else
+        "sim_kernels": ("k_sims32w<%d> for every simulation step of the window: one workgroup per game runs its backup, "
+                        "select, expand and network evaluation with no grid-wide step boundary; the roofline / "
+                        "tree_walk events come from a %d-step profile pass after the timed window, whose every-32nd "
+                        "steps run as separate kernels" % (args.filters, tm["profile_sim_steps"])
+                        ) if tm.get("persistent") else
                        "k_step (backup + select + expand) + the fused tower, two launches per simulation step",
         "evals_per_sim": evals_all / max(sims_all, 1),
         "terminal_leaf_frac": term_all / max(sims_all, 1),
