@@ -138,6 +138,8 @@ struct NetDev {
     bool winograd = AZ_WINOGRAD_DEFAULT != 0;   // tower32w_kernel for f32 F >= 64 nets (env AZ_WINOGRAD=0/1)
     float* head = nullptr;          // folded head weights (f32)
     void* head_frag = nullptr;      // 1x1 F->40 head conv as bf16 hi/lo MFMA A-fragments (fused tower)
+    void* in_pk32 = nullptr;        // f32 Winograd nets: the input conv's weights with channels 16-18 of 4 taps packed per k-step (tower32w)
+    size_t in_pk32_bytes = 0;
     void* head_frag32 = nullptr;    // the same conv as f32 A-fragments of v_mfma_f32_16x16x4_f32 (f32 fused tower)
     size_t head_floats = 0;
     hipStream_t stream = nullptr;

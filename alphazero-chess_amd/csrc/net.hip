@@ -430,6 +430,27 @@ std::vector<float> swizzle_f32(const std::vector<float>& wf, int cout, int cin_r
     return o;
 }
 
+// The f32 input conv (19 planes) for the Winograd tower, packed: k-steps 0-8 = tap k, channels
+// 0-15 (lane group h: channels 4h..4h+3, component = the MFMA k-slice); k-steps 9-11: slice s of
+// k-step 9 + kl = tap 4 kl + s, lane group h = channel 16 + h (channel 19 and taps >= 9 zero);
+// then 8 zero k-steps (ring refills past the end).  12 k-steps instead of the 18 of 32 padded
+// channels (tower.hip conv32_in_packed)
+std::vector<float> swizzle_f32_input_packed(const std::vector<float>& wf, int cout) {
+    const int CF = cout / 16, NK = 12;
+    std::vector<float> o((size_t)(NK + 8) * CF * 64 * 4, 0.0f);
+    for (int k = 0; k < NK; k++)
+        for (int cf = 0; cf < CF; cf++)
+            for (int lane = 0; lane < 64; lane++)
+                for (int s = 0; s < 4; s++) {
+                    const int co = cf * 16 + (lane & 15), h = lane >> 4;
+                    const int tap = k < 9 ? k : 4 * (k - 9) + s;
+                    const int ci = k < 9 ? 4 * h + s : 16 + h;
+                    o[(((size_t)k * CF + cf) * 64 + lane) * 4 + s] =
+                        (tap < 9 && ci < 19) ? wf[((size_t)co * 19 + ci) * 9 + tap] : 0.0f;
+                }
+    return o;
+}
+
 // Winograd F(2x2,3x3) weights U = G g G^T (f64, rounded once), fragment-swizzled for the MFMA A
 // operand: [ci/16][xi][co/16][lane][4], lane = co%16 + 16*((ci%16)/4), component ci%4, then 8 zero
 // steps (ring refills past the end); tap = dy*3 + dx as in swizzle_f32
@@ -494,6 +515,12 @@ int net_create(const az_net_desc* d, const float* wts, size_t n, int device, Net
             if (hipMemcpy(dw, s.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) return -1;
         }
         net->conv_bytes.push_back(bytes);
+        if (d->dtype == AZ_DTYPE_F32 && F >= 64 && cin == 19) {  // packed input conv for tower32w_kernel
+            auto u = swizzle_f32_input_packed(wf, F);
+            if (hipMalloc(&net->in_pk32, u.size() * 4) != hipSuccess) return -1;
+            if (hipMemcpy(net->in_pk32, u.data(), u.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return -1;
+            net->in_pk32_bytes = u.size() * 4;
+        }
         if (d->dtype == AZ_DTYPE_F32 && F >= 64 && cin == F) {   // Winograd F(2x2,3x3) copy for tower32w_kernel
             auto u = winograd_f32(wf, F);
             void* du = nullptr;
@@ -598,6 +625,7 @@ void net_destroy(NetDev* n) {
     (void)hipFree(n->head);
     (void)hipFree(n->head_frag);
     (void)hipFree(n->head_frag32);
+    (void)hipFree(n->in_pk32);
     (void)hipFree(n->x); (void)hipFree(n->h); (void)hipFree(n->planes);
     (void)hipFree(n->d_in); (void)hipFree(n->d_pol); (void)hipFree(n->d_val);
     if (n->stream) (void)hipStreamDestroy(n->stream);

@@ -39,6 +39,8 @@ struct TowerArgs {
     unsigned wbytes[1 + 2 * 40];   // allocation bytes of each w[i] (buffer-load range check)
     const uint4* ww[2 * 40];       // f32 Winograd weights of the residual convs (F = 256, tower32w_kernel)
     unsigned wwbytes[2 * 40];
+    const uint4* w0pk;             // the input conv packed for tower32w_kernel (net.hip swizzle_f32_input_packed)
+    unsigned w0pk_bytes;
     int blocks;
 };
 
@@ -247,8 +249,9 @@ template <int F, int RS, int NB, int NT, bool SEARCH, bool F32X = false>
 __device__ __forceinline__ void heads_group(const char* __restrict__ xb, float* __restrict__ scr, int b0, int nb,
                                             int row0, int tid, const uint4* __restrict__ hfrag,
                                             const float* __restrict__ head, float* pol_out, float* val_out,
-                                            const SearchOut& so) {
+                                            const SearchOut& so, unsigned long long* tr = nullptr) {
     constexpr int NPART = heads_npart(NT, F32X);
+    wino_stamp(tr, 1900);
     typedef HeadsScratch<NB, NT, NPART> S;
     constexpr int NW = S::NW, PV = S::PV, P1S = HEADS_P1S;
     const HeadLayout L = HeadLayout::make(F);
@@ -305,6 +308,30 @@ __device__ __forceinline__ void heads_group(const char* __restrict__ xb, float* 
 #pragma unroll
         for (int i = 0; i < KPRE; i++) wv[i] = head[L.l1w + (size_t)(w * KP + i) * 64 + lane];
     }
+    // biases of A, B and the value head, and (search mode) the new node's record: requested here,
+    // behind the weight prefetches, so that no phase ends on a dependent global load (C2 heads
+    // stamps: ~1-2k cycles each)
+    f32x4 b40v[3];
+#pragma unroll
+    for (int cf = 0; cf < 3; cf++) b40v[cf] = *reinterpret_cast<const f32x4*>(head + L.b40 + cf * 16 + 4 * h);
+    f32x4 p2bv[TPW > 0 ? TPW : 1];
+#pragma unroll
+    for (int k = 0; k < TPW; k++)
+        p2bv[k] = *reinterpret_cast<const f32x4*>(head + L.p2b + ((w + k * NW) >> 2 & 3) * 16 + 4 * h);
+    const float l1bv = head[L.l1b + lane], l2wv = head[L.l2w + lane], l2bv = head[L.l2b];
+    int sgame[NB], snode[NB];
+    Node snd[NB];
+    if constexpr (SEARCH) {
+#pragma unroll
+        for (int bb = 0; bb < NB; bb++) {
+            if (b0 + bb < nb) {
+                const int row = vgpr_index(row0 + b0 + bb);
+                sgame[bb] = so.row_game[row];
+                snode[bb] = so.row_node[row];
+                snd[bb] = so.nodes[(size_t)sgame[bb] * so.NMAX + snode[bb]];
+            }
+        }
+    }
     // A
     for (int sfr = w; sfr < 4 * NB; sfr += NW) {
         const int bb = sfr >> 2, sq = (sfr & 3) * 16 + l16;
@@ -353,10 +380,12 @@ __device__ __forceinline__ void heads_group(const char* __restrict__ xb, float* 
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 const int ch = cf * 16 + 4 * h + r;
-                if (ch < 40) p1v1[bb * PV + ch * P1S + sq] = fmaxf(acc[cf][r] + head[L.b40 + ch], 0.0f);
+                if (ch < 40) p1v1[bb * PV + ch * P1S + sq] = fmaxf(acc[cf][r] + b40v[cf][r], 0.0f);
             }
     }
+    wino_stamp(tr, 1901);
     __syncthreads();
+    wino_stamp(tr, 1902);
     // B
     float mxb[NB];
 #pragma unroll
@@ -372,7 +401,7 @@ __device__ __forceinline__ void heads_group(const char* __restrict__ xb, float* 
 #pragma unroll
         for (int r = 0; r < 4; r++) {
             const int c2 = cf * 16 + 4 * h + r;
-            const float l = acc[r] + head[L.p2b + c2];
+            const float l = acc[r] + p2bv[k][r];
             lg[bb * 4096 + c2 * 64 + sf * 16 + l16] = l;
 #pragma unroll
             for (int q = 0; q < NB; q++)
@@ -411,7 +440,9 @@ __device__ __forceinline__ void heads_group(const char* __restrict__ xb, float* 
         const float m = t_wave_max(mxb[bb]);
         if (lane == 0) stat[bb * (2 * NW + 4) + w] = m;
     }
+    wino_stamp(tr, 1903);
     __syncthreads();
+    wino_stamp(tr, 1904);
     float mx[NB];
 #pragma unroll
     for (int bb = 0; bb < NB; bb++) {
@@ -425,10 +456,10 @@ __device__ __forceinline__ void heads_group(const char* __restrict__ xb, float* 
     }
     if (w < NB) {                                       // wave bb finishes board bb's value head
         const int bb = w;
-        float hs = head[L.l1b + lane];
+        float hs = l1bv;
         for (int i = 0; i < NW * NPART; i++) hs += red[(bb * NW * NPART + i) * 64 + lane];
-        float hv = t_wave_sum(fmaxf(hs, 0.0f) * head[L.l2w + lane]);
-        if (lane == 0) stat[bb * (2 * NW + 4) + 2 * NW] = tanhf(hv + head[L.l2b]);
+        float hv = t_wave_sum(fmaxf(hs, 0.0f) * l2wv);
+        if (lane == 0) stat[bb * (2 * NW + 4) + 2 * NW] = tanhf(hv + l2bv);
     }
     if constexpr (SEARCH) {                             // thread 0 reserves eval-log slots
         if (tid == 0 && so.log_cap > 0) {
@@ -437,9 +468,7 @@ __device__ __forceinline__ void heads_group(const char* __restrict__ xb, float* 
                 int* sl = reinterpret_cast<int*>(stat + bb * (2 * NW + 4) + 2 * NW + 1);
                 sl[0] = -1;
                 if (b0 + bb >= nb) continue;
-                const int row = vgpr_index(row0 + b0 + bb);
-                const int game = so.row_game[row], node = so.row_node[row];
-                const Node nd = so.nodes[(size_t)game * so.NMAX + node];
+                const Node nd = snd[bb];
                 const int r = atomicAdd(&so.ctr->log_count, 1);
                 const int po = atomicAdd(&so.ctr->log_prior_count, (int)nd.nedges);
                 sl[0] = (r < so.log_cap && po + nd.nedges <= so.log_prior_cap) ? r : -1;
@@ -447,7 +476,9 @@ __device__ __forceinline__ void heads_group(const char* __restrict__ xb, float* 
             }
         }
     }
+    wino_stamp(tr, 1905);
     __syncthreads();
+    wino_stamp(tr, 1906);
 #pragma unroll
     for (int bb = 0; bb < NB; bb++) {
         if (b0 + bb >= nb) break;
@@ -462,8 +493,8 @@ __device__ __forceinline__ void heads_group(const char* __restrict__ xb, float* 
             for (int i = tid; i < 4096; i += NT) pr[i] = expf(lb[i] - mx[bb]) / sum;
             if (tid == 0) val_out[row] = value;
         } else {
-            const int game = so.row_game[row], node = so.row_node[row];
-            const Node nd = so.nodes[(size_t)game * so.NMAX + node];
+            const int game = sgame[bb], node = snode[bb];
+            const Node nd = snd[bb];
             Edge* e = so.edges + (size_t)game * so.EMAX + nd.edge_begin;
             const int* sl = reinterpret_cast<const int*>(st + 2 * NW + 1);
             const int slot = so.log_cap > 0 ? sl[0] : -1;
@@ -701,6 +732,104 @@ __device__ __forceinline__ void conv32_lds(const char* __restrict__ ldsb, char* 
     __syncthreads();
 }
 
+// The f32 input conv of the Winograd tower (19 planes -> F, one board): the weights packed by
+// net.hip swizzle_f32_input_packed -- k-steps 0-8: tap k, channels 0-15 (one ds_read_b128 of
+// B per square fragment feeds 4 MFMAs, as conv32_lds); k-steps 9-11: MFMA slice s = tap 4 kl + s,
+// lane group h = channel 16 + h (one ds_read_b32 per slice and square fragment).  12 k-steps of
+// MFMAs instead of conv32_lds's 18 over 32 zero-padded channels.  Input planes at in_off (row
+// stride RSI slots, channels 0-31), output F channels at outb (row stride RSO), + bias, ReLU.
+// wr holds k-steps [0, T32_PF) on entry; rW covers the 12 k-steps and the 8 zero ones after.
+template <int F, int RSI, int RSO, int NCO>
+__device__ __forceinline__ void conv32_in_packed(const char* __restrict__ ldsb, char* __restrict__ outb, int in_off,
+                                                 int zero_off, const __amdgpu_buffer_rsrc_t rW,
+                                                 const float* __restrict__ bias, f32x4 (&wr)[T32_PF][NCO], int cw,
+                                                 int lane) {
+    constexpr int CF = F / 16, MF = 4, PF = T32_PF, KB = CF * 64 * 16, NK = 12;
+    static_assert(NK % PF == 0, "ring slots must be compile-time");
+    const int h = lane >> 4, l16 = lane & 15;
+    f32x4 acc[MF][NCO];
+#pragma unroll
+    for (int n = 0; n < NCO; n++) {
+        const float4 bn = *reinterpret_cast<const float4*>(bias + cw * 16 * NCO + n * 16 + h * 4);
+#pragma unroll
+        for (int m = 0; m < MF; m++) acc[m][n] = f32x4{bn.x, bn.y, bn.z, bn.w};
+    }
+    const int voff = ((cw * NCO) * 64 + lane) * 16;
+    const int lr = l16 >> 3, lf = l16 & 7;
+    // square fragment m, tap: the lane's square (2 m + lr, lf) shifted by the tap; off-board taps
+    // read the zero row (channels 0-15: at the same slot mod 16, conflict-free as conv32_lds)
+    auto tap_ok = [&](int tap, int m) {
+        const int dr = tap / 3 - 1, df = tap % 3 - 1;
+        return (unsigned)(lf + df) < 8u && (unsigned)(2 * m + lr + dr) < 8u;
+    };
+    auto row_addr = [&](int tap, int m) {   // byte offset of the shifted square's row
+        const int dr = tap / 3 - 1, df = tap % 3 - 1;
+        return ((l16 + m * 16 + dr * 8 + df) * RSI) * 16 + in_off;
+    };
+    auto main_addr = [&](int tap, int m) {
+        const int va = row_addr(tap, m) + h * 16;
+        return tap_ok(tap, m) ? va : ((va & 0xF0) | zero_off);
+    };
+    auto side_addr = [&](int tap, int m) {  // channel 16 + h
+        return tap_ok(tap, m) ? row_addr(tap, m) + 64 + h * 4 : zero_off + 64 + h * 4;
+    };
+    f32x4 bq[MF];
+#pragma unroll
+    for (int m = 0; m < MF; m++) bq[m] = *reinterpret_cast<const f32x4*>(ldsb + main_addr(0, m));
+#pragma unroll
+    for (int k = 0; k < NK; k++) {
+        // next k-step's B fragments first: a whole k-step of MFMAs covers their latency
+        f32x4 bn[MF];
+        if (k + 1 < 9) {
+#pragma unroll
+            for (int m = 0; m < MF; m++) bn[m] = *reinterpret_cast<const f32x4*>(ldsb + main_addr(k + 1, m));
+        } else if (k + 1 < NK) {
+            const int kl = k + 1 - 9;
+#pragma unroll
+            for (int m = 0; m < MF; m++)
+#pragma unroll
+                for (int s4 = 0; s4 < 4; s4++) {
+                    const int tap = 4 * kl + s4;
+                    bn[m][s4] = tap < 9 ? *reinterpret_cast<const float*>(ldsb + side_addr(tap, m)) : 0.0f;
+                }
+        }
+        f32x4 a[NCO];
+#pragma unroll
+        for (int n = 0; n < NCO; n++) a[n] = wr[k % PF][n];
+#pragma unroll
+        for (int n = 0; n < NCO; n++)
+            wr[k % PF][n] = __builtin_bit_cast(
+                f32x4, __builtin_amdgcn_raw_buffer_load_b128(rW, voff + n * 1024 + (k + PF) * KB, 0, 0));
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; s4++)
+#pragma unroll
+            for (int m = 0; m < MF; m++)
+#pragma unroll
+                for (int n = 0; n < NCO; n++)
+                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[n][s4], bq[m][s4], acc[m][n], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (k + 1 < NK) {
+#pragma unroll
+            for (int m = 0; m < MF; m++) bq[m] = bn[m];
+        }
+    }
+    // epilogue: + ReLU, 4 consecutive channels of one square per lane; the barrier after publishes it
+#pragma unroll
+    for (int n = 0; n < NCO; n++) {
+        const int co = cw * 16 * NCO + n * 16 + h * 4;
+        char* lane_base = outb + (l16 * RSO + (co >> 2)) * 16;
+#pragma unroll
+        for (int m = 0; m < MF; m++) {
+            f32x4 v = acc[m][n];
+#pragma unroll
+            for (int r = 0; r < 4; r++) v[r] = fmaxf(v[r], 0.0f);
+            *reinterpret_cast<f32x4*>(lane_base + (m * 16) * RSO * 16) = v;
+        }
+    }
+    __syncthreads();
+}
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t t32_rsrc(const uint4* p, unsigned bytes) {
     return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, 0x00020000);
 }
@@ -924,10 +1053,9 @@ __device__ __forceinline__ void tower32w_board(const float* __restrict__ planes,
     }
     __syncthreads();
     wino_stamp(tr, 1);
-    {   // input conv 19 (32) -> F: direct (18 k-steps)
+    {   // input conv 19 -> F: direct, channels 16-18 of four taps packed per k-step (12 k-steps)
         f32x4 wr[T32_PF][NN];
-        const __amdgpu_buffer_rsrc_t r0 = t32_rsrc(ta.w[0], ta.wbytes[0]);
-        const __amdgpu_buffer_rsrc_t rz = t32_rsrc(ta.w[0] + 18 * (F / 16) * 64, ta.wbytes[0] - 18 * (F / 16) * 1024);
+        const __amdgpu_buffer_rsrc_t r0 = t32_rsrc(ta.w0pk, ta.w0pk_bytes);
         const int voff = ((w * NN) * 64 + lane) * 16;
 #pragma unroll
         for (int i = 0; i < T32_PF; i++)
@@ -935,8 +1063,7 @@ __device__ __forceinline__ void tower32w_board(const float* __restrict__ planes,
             for (int n = 0; n < NN; n++)
                 wr[i][n] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                                          r0, voff + n * 1024 + i * (F / 16) * 1024, 0, 0));
-        conv32_lds<32, RSI, F, RSF, 1, NN, false>(ldsb, reinterpret_cast<char*>(X), vbase, zero_off, r0, rz, ta.b[0],
-                                                  wr, w, 0, lane);
+        conv32_in_packed<F, RSI, RSF, NN>(ldsb, reinterpret_cast<char*>(X), vbase, zero_off, r0, ta.b[0], wr, w, lane);
     }
     wino_stamp(tr, 2);
     f32x4 xres[NN][4];
@@ -975,7 +1102,7 @@ __device__ __forceinline__ void tower32w_board(const float* __restrict__ planes,
                            F == 64 ? 1 : 0, flag, 2 * b + 2, tr ? tr + 35 + 64 * b : nullptr);
     }
     heads_group<F, RSF, 1, NT, SEARCH, true>(ldsb, reinterpret_cast<float*>(V), 0, 1, row0, tid, ta.head_frag32, ta.head,
-                                             pol_out, val_out, so);
+                                             pol_out, val_out, so, tr);
     wino_stamp(tr, 3 + 64 * 20);
 }
 
@@ -1015,16 +1142,21 @@ k_sims32w(Engine E, TowerArgs ta, SearchOut so, int step0, int step1) {
         // arithmetic is hoisted across the other (it would stay live through it and spill)
         const int tid = vgpr_index(threadIdx.x), g = vgpr_index(blockIdx.x);
         const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+        unsigned long long* tr = tt_slot(w);            // trace builds only (nullptr otherwise)
+        wino_stamp(tr, 1910);
         if (w == 0) {
             if (step > step0) {                        // the previous simulation's backup
                 backup_game(E, g, lane);
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
             }
+            wino_stamp(tr, 1911);
             int kind = X_NONE, nid = -1;
             if (step < step1) {
                 select_game(E, g, lane);
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                wino_stamp(tr, 1912);
                 kind = expand_leaf_wave<1>(E, g, lane, &nid, step);   // wave 0 only
+                wino_stamp(tr, 1913);
                 if (lane == 0) {
                     if (kind == X_ROW) {
                         E.row_game[g] = g;
@@ -1043,11 +1175,13 @@ k_sims32w(Engine E, TowerArgs ta, SearchOut so, int step0, int step1) {
         }
         __syncthreads();
         const int kind = s_kind;
+        wino_stamp(tr, 1914);
         if (kind == X_ROW) {
             if constexpr (BF16) tower_board<F, true>(nullptr, ta, g, 1, nullptr, nullptr, so, tid);
             else tower32w_board<F, true>(nullptr, ta, g, nullptr, nullptr, so, tid);
         }
         __syncthreads();
+        wino_stamp(tr, 1915);
     }
 }
 
@@ -1057,7 +1191,8 @@ bool tower_supported(const NetDev* n) {
 }
 
 bool wino_supported(const NetDev* n) {
-    return n->dtype == AZ_DTYPE_F32 && n->winograd && n->filters >= 64 && (int)n->wino_w.size() == 2 * n->blocks;
+    return n->dtype == AZ_DTYPE_F32 && n->winograd && n->filters >= 64 && (int)n->wino_w.size() == 2 * n->blocks &&
+           n->in_pk32 != nullptr;
 }
 
 static TowerArgs tower_args(const NetDev* n) {
@@ -1075,6 +1210,8 @@ static TowerArgs tower_args(const NetDev* n) {
         ta.ww[i] = reinterpret_cast<const uint4*>(n->wino_w[i]);
         ta.wwbytes[i] = (unsigned)n->wino_bytes[i];
     }
+    ta.w0pk = reinterpret_cast<const uint4*>(n->in_pk32);
+    ta.w0pk_bytes = (unsigned)n->in_pk32_bytes;
     ta.blocks = n->blocks;
     return ta;
 }

@@ -23,3 +23,17 @@ for n, a, b in ph:
     print("  %-38s %7.0f" % (n, (conv[..., b] - conv[..., a]).mean()))
 print("  between convs (epilogue barrier)       %7.0f" % (conv[..., 1:, 0] - conv[..., :-1, 11]).mean())
 print("MFMA per wave per conv: 256 x 32 = 8192 cycles")
+
+h = t[:, :, 1900:1907]
+hn = ["weights + 1x1 conv (A)", "barrier", "policy conv + value FC (B, C)", "barrier", "softmax sum + value",
+      "barrier"]
+print("heads:")
+for k in range(6):
+    print("  %-38s %7.0f" % (hn[k], (h[..., k + 1] - h[..., k]).mean()))
+print("  %-38s %7.0f" % ("priors + value out", (t[:, :, end] - h[..., 6]).mean()))
+s0 = t[:, 0, 1910:1916]
+if (s0 > 0).all():
+    print("simulation (wave 0, last simulation of the traced games):")
+    for n, a, b in [("backup", 0, 1), ("select", 1, 2), ("expand", 2, 3), ("to the tower (barrier)", 3, 4),
+                    ("tower + barrier", 4, 5)]:
+        print("  %-38s %7.0f" % (n, (s0[:, b] - s0[:, a]).mean()))
