@@ -33,7 +33,7 @@ PEAK_F32_TFLOPS = 157.3       # MI355X_MICROARCH.md: f32 MFMA = vector peak
 PEAK_HBM_GBS = 8000.0         # MI355X_MICROARCH.md: 8.0 TB/s spec
 # HBM bytes per tower launch from rocprofv3 PMC passes (tools/pmc_run.sh: FETCH_SIZE x2 per the
 # gfx950 correction + WRITE_SIZE), same kernel and per-launch work (2048 rows, 20x256)
-PMC_SUMMARY = {"f32": os.path.join(ROOT, "profiles", "r03_pmc_tower32w_5_summary.json"),           # Winograd
+PMC_SUMMARY = {"f32": os.path.join(ROOT, "profiles", "r03_pmc_tower32w_8_summary.json"),           # Winograd
                "f32-direct": os.path.join(ROOT, "profiles", "r02_pmc_tower32_summary.json"),      # AZ_WINOGRAD=0
                "bf16": os.path.join(ROOT, "profiles", "r01_pmc_tower_v11_summary.json")}
 # simulation steps of the instrumented profile pass after the timed window (8 sampled tower launches)
@@ -195,14 +195,16 @@ def tower_algo_flop_per_row(B, F):
 
 
 def tower_exec_flop_per_row(B, F, dtype, wino):
-    """MFMA FLOPs the fused tower issues per row: the input conv with its 19 input planes padded to
-    32 channels, the residual convs (Winograd: 16 points x 16 tiles x F x F per conv; direct: 64
+    """MFMA FLOPs the fused tower issues per row: the input conv (direct towers: 19 input planes
+    padded to 32 channels, 18 k-steps of 16; Winograd towers: channels 16-18 of four taps packed per
+    k-step, 12 k-steps of 16 -- tower.hip conv32_in_packed), the residual convs (Winograd: 16 points x 16 tiles x F x F per conv; direct: 64
     squares x 9 taps x F x F), the heads' 1x1 F->40 conv padded to 48 rows (bf16 mode: split into
     hi + lo bf16 fragments, twice the MFMAs) and the 32->64 policy conv.  The value MLP runs on
     VALU.  Cross-check: PMC SQ_INSTS_MFMA x 2048 FLOP (profiles/*pmc*summary.json)."""
     res = (16.0 * 16.0 if (wino and dtype != "bf16") else 64.0 * 9.0) * 2.0 * F * F * 2 * B
     heads = 2.0 * 64.0 * 48.0 * F * (2 if dtype == "bf16" else 1) + 2.0 * 64.0 * 64.0 * 32.0
-    return 2.0 * 64.0 * 9.0 * 32.0 * F + res + heads
+    inconv = 2.0 * 64.0 * 16.0 * (12.0 if (wino and dtype != "bf16") else 18.0) * F
+    return inconv + res + heads
 
 
 def config_name(games, sims, blocks, filters):
@@ -526,7 +528,8 @@ def main():
                              if tm["persistent"] else "of the timed window"),
                 "executed_flop_per_row": exec_row,
                 "executed_note": ("Winograd F(2x2,3x3): the residual convs execute 1/2.25 of the direct-conv "
-                                  "multiplies; input conv (19 -> 32 padded channels) and the heads' MFMAs included"
+                                  "multiplies; input conv (19 planes in 12 packed k-steps) and the heads' MFMAs "
+                                  "included"
                                   if wino else "direct convolution, input channels padded 19 -> 32, heads included"),
                 "algorithmic_tflops": algo_tflops,
                 "algorithmic_note": "direct-conv FLOPs of SURVEY 8a A6 (no heads) / tower time: an equivalent rate",
