@@ -1,0 +1,9 @@
+# round 3: chunk-0 pre-transform split over all 8 waves (own item each, AZ_PRE8) instead of two
+# items per leading wave: C3 A/B against the default build, then net/search tests on the variant
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 500 bash tools/ab_run.sh gpurun_out/r03_ab_pre8_c3.log 32 alphazero-chess_amd/azchess/libaz.so build_var/pre8/libaz.so alphazero-chess_amd/azchess/libaz.so build_var/pre8/libaz.so || exit 3
+grep move gpurun_out/r03_ab_pre8_c3.log | cut -c1-160
+cp build_var/pre8/libaz.so alphazero-chess_amd/azchess/libaz.so
+timeout -k 10 300 python -u -m pytest tests/test_gpu_net.py tests/test_gpu_search.py -m gpu -q --timeout 200 --timeout-method thread > gpurun_out/r03_pre8_tests.log 2>&1; rc=$?
+tail -3 gpurun_out/r03_pre8_tests.log; exit $rc
