@@ -34,6 +34,7 @@ print("  %-38s %7.0f" % ("priors + value out", (t[:, :, end] - h[..., 6]).mean()
 s0 = t[:, 0, 1910:1916]
 if (s0 > 0).all():
     print("simulation (wave 0, last simulation of the traced games):")
-    for n, a, b in [("backup", 0, 1), ("select", 1, 2), ("expand", 2, 3), ("to the tower (barrier)", 3, 4),
-                    ("tower + barrier", 4, 5)]:
+    # the kernel's last loop iteration only backs up (no select / expand): its 1912 / 1913 stamps are
+    # the previous simulation's, so only intervals within one iteration are printed
+    for n, a, b in [("backup", 0, 1), ("expand", 2, 3)]:
         print("  %-38s %7.0f" % (n, (s0[:, b] - s0[:, a]).mean()))
