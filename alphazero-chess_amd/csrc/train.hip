@@ -230,6 +230,84 @@ wgrad_f32_kernel(const float* __restrict__ X, int ldx, int K, const float* __res
             }
 }
 
+// Winograd weight-grad GEMM at F = 256: one workgroup per (row split, point xi) computes the whole
+// 256 x 256 dU[xi] partial over its (board, tile) rows, so each transformed operand is read from
+// HBM once (64 x 64 tiles read each four times and were bound by that traffic).  8 waves, wave w
+// owns co [32 w, 32 w + 32) x all 256 ci: accumulator block (j, c) row m is ci = 64 j + 4 m + c, so
+// one ds_read_b128 of a row feeds four blocks; 32 MFMAs per 4 LDS b128 + 2 b32 reads per 4 rows.
+// Rows are staged WG_R at a time through LDS, the next stage's prefetched into registers beside
+// the current stage's MFMAs.  partial[split][xi][ci][co]; every element sums its split's rows in
+// row order (fixed order; splits reduced in order by reduce_kernel).
+constexpr int WG_R = 32, WG_S = 256 + 16;
+__global__ void __launch_bounds__(512)
+wino_wgrad_gemm_kernel(const float* __restrict__ Vt, const float* __restrict__ Mt, int K, int rows_per_split,
+                       float* __restrict__ partial) {
+    constexpr int F = 256, NV = WG_R * (F / 4) / 512;
+    __shared__ __attribute__((aligned(16))) float xs[WG_R * WG_S];
+    __shared__ __attribute__((aligned(16))) float ds[WG_R * WG_S];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int split = blockIdx.x, xi = blockIdx.y;
+    const float* X = Vt + (size_t)xi * K * F;
+    const float* D = Mt + (size_t)xi * K * F;
+    const int rbeg = split * rows_per_split, rend = min(K, rbeg + rows_per_split);
+    f32x4 acc[16][2];
+#pragma unroll
+    for (int b = 0; b < 16; b++)
+#pragma unroll
+        for (int n = 0; n < 2; n++) acc[b][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float4 xv[NV], dv[NV];
+    auto fetch = [&](int rc) {
+#pragma unroll
+        for (int j = 0; j < NV; j++) {
+            const int i = tid + j * 512, rr = i >> 6, c4 = (i & 63) * 4;
+            xv[j] = dv[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (rc + rr < rend) {
+                xv[j] = *reinterpret_cast<const float4*>(X + (size_t)(rc + rr) * F + c4);
+                dv[j] = *reinterpret_cast<const float4*>(D + (size_t)(rc + rr) * F + c4);
+            }
+        }
+    };
+    if (rbeg < rend) fetch(rbeg);
+    for (int rc = rbeg; rc < rend; rc += WG_R) {
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < NV; j++) {
+            const int i = tid + j * 512, rr = i >> 6, c4 = (i & 63) * 4;
+            *reinterpret_cast<float4*>(xs + rr * WG_S + c4) = xv[j];
+            *reinterpret_cast<float4*>(ds + rr * WG_S + c4) = dv[j];
+        }
+        __syncthreads();
+        if (rc + WG_R < rend) fetch(rc + WG_R);
+#pragma unroll 2
+        for (int q = 0; q < WG_R / 4; q++) {
+            const int rq = q * 4 + (lane >> 4);
+            const float b0 = ds[rq * WG_S + 32 * w + (lane & 15)];
+            const float b1 = ds[rq * WG_S + 32 * w + 16 + (lane & 15)];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const f32x4 a = *reinterpret_cast<const f32x4*>(xs + rq * WG_S + 64 * j + 4 * (lane & 15));
+#pragma unroll
+                for (int c = 0; c < 4; c++) {
+                    acc[4 * j + c][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c], b0, acc[4 * j + c][0], 0, 0, 0);
+                    acc[4 * j + c][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c], b1, acc[4 * j + c][1], 0, 0, 0);
+                }
+            }
+        }
+    }
+    float* out = partial + ((size_t)split * 16 + xi) * F * F;
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+#pragma unroll
+            for (int n = 0; n < 2; n++)
+#pragma unroll
+                for (int g = 0; g < 4; g++) {
+                    const int ci = 64 * j + 4 * (4 * (lane >> 4) + g) + c, co = 32 * w + 16 * n + (lane & 15);
+                    out[(size_t)ci * F + co] = acc[4 * j + c][n][g];
+                }
+}
+
 // out[e] = sum over splits s (in order) of partial[s][e]
 __global__ void reduce_kernel(const float* __restrict__ partial, int splits, size_t n, float* __restrict__ out) {
     for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
@@ -838,16 +916,27 @@ int launch_wgrad(Trainer* T, int taps, const float* X, int ldx, int K, const flo
 // Winograd weight grad of a residual F x F conv (input X, output gradient DY, B boards) into g
 int wino_rows_per_split(int B) { return B * 16 >= 8192 ? WINO_ROWS_PER_SPLIT : ROWS_PER_SPLIT; }
 size_t wino_splits(int B) { return (size_t)((B * 16 + wino_rows_per_split(B) - 1) / wino_rows_per_split(B)); }
+// F = 256 (wino_wgrad_gemm_kernel): 512 rows per split, 16 x 16 = 256 workgroups at B = 512
+constexpr int WINO_GEMM_ROWS = 512;
+size_t wino_gemm_splits(int B) { return (size_t)((B * 16 + WINO_GEMM_ROWS - 1) / WINO_GEMM_ROWS); }
 int launch_wino_wgrad(Trainer* T, const float* X, const float* DY, int B, float* g) {
     const int F = T->F, K = B * 16;
     if (B > T->Bmax) return fail("Winograd wgrad: batch too large");
     if (wino_splits(B) * 16 * (size_t)F * F > T->wpart_cap) return fail("Winograd wgrad: partial buffer too small");
     hipStream_t st = T->st;
     tr::wino_wgrad_transform_kernel<<<grid_for((size_t)K * F), 256, 0, st>>>(X, DY, F, B, T->wvt, T->wmt);
-    const int rps = wino_rows_per_split(B), splits = (int)wino_splits(B);
-    dim3 grid(F / tr::GK, F / tr::GN, splits * 16);
-    tr::wgrad_f32_kernel<1><<<grid, 256, 0, st>>>(T->wvt, F, F, T->wmt, F, F, K, rps, T->wpart, 16, (size_t)K * F,
-                                                  (size_t)K * F);
+    int splits;
+    if (F == 256) {
+        splits = (int)wino_gemm_splits(B);
+        if (splits * 16 * (size_t)F * F > T->wpart_cap) return fail("Winograd wgrad: partial buffer too small");
+        tr::wino_wgrad_gemm_kernel<<<dim3(splits, 16), 512, 0, st>>>(T->wvt, T->wmt, K, WINO_GEMM_ROWS, T->wpart);
+    } else {
+        const int rps = wino_rows_per_split(B);
+        splits = (int)wino_splits(B);
+        dim3 grid(F / tr::GK, F / tr::GN, splits * 16);
+        tr::wgrad_f32_kernel<1><<<grid, 256, 0, st>>>(T->wvt, F, F, T->wmt, F, F, K, rps, T->wpart, 16, (size_t)K * F,
+                                                      (size_t)K * F);
+    }
     const size_t n = (size_t)16 * F * F;
     tr::reduce_kernel<<<grid_for(n), 256, 0, st>>>(T->wpart, splits, n, T->wdu);
     tr::wino_wgrad_out_kernel<<<grid_for((size_t)F * F), 256, 0, st>>>(T->wdu, F, g);
@@ -1147,7 +1236,7 @@ int az_trainer_create(int blocks, int filters, const float* weights, size_t n, i
     wp = std::max(wp, s1 * 32 * 64);                                    // policy_conv_2
     wp = std::max(wp, sl * 512 * 64);                                   // value_linear_1
     if (T->wino) {   // Winograd weight grads: [16][Bmax * 16][F] transforms, dU [16][F][F]
-        wp = std::max(wp, wino_splits(max_batch) * 16 * (size_t)F * F);
+        wp = std::max(wp, std::max(wino_splits(max_batch), wino_gemm_splits(max_batch)) * 16 * (size_t)F * F);
         T->wvt = A((size_t)16 * max_batch * 16 * F);
         T->wmt = A((size_t)16 * max_batch * 16 * F);
         T->wdu = A((size_t)16 * F * F);
