@@ -238,7 +238,7 @@ wgrad_f32_kernel(const float* __restrict__ X, int ldx, int K, const float* __res
 // Rows are staged WG_R at a time through LDS, the next stage's prefetched into registers beside
 // the current stage's MFMAs.  partial[split][xi][ci][co]; every element sums its split's rows in
 // row order (fixed order; splits reduced in order by reduce_kernel).
-constexpr int WG_R = 32, WG_S = 256 + 16;
+constexpr int WG_R = 16, WG_S = 256 + 16;   // 16 rows per stage: 142 us vs 146 (32), 151 (64), 146 (8)
 __global__ void __launch_bounds__(512)
 wino_wgrad_gemm_kernel(const float* __restrict__ Vt, const float* __restrict__ Mt, int K, int rows_per_split,
                        float* __restrict__ partial) {
@@ -278,7 +278,7 @@ wino_wgrad_gemm_kernel(const float* __restrict__ Vt, const float* __restrict__ M
         }
         __syncthreads();
         if (rc + WG_R < rend) fetch(rc + WG_R);
-#pragma unroll 2
+#pragma unroll
         for (int q = 0; q < WG_R / 4; q++) {
             const int rq = q * 4 + (lane >> 4);
             const float b0 = ds[rq * WG_S + 32 * w + (lane & 15)];
