@@ -6,6 +6,8 @@ time -- there is no Python or CPU fallback for any compute entry point.
 import ctypes as C
 import os
 
+import numpy as np
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # AZ_LIB selects an alternative in-tree build of the same ABI (kernel-variant A/B runs)
 LIB_PATH = os.environ.get("AZ_LIB") or os.path.join(_HERE, "libaz.so")
@@ -22,6 +24,13 @@ class AzPos(C.Structure):
     _fields_ = [("bb", C.c_uint64 * 8), ("turn", C.c_uint8), ("castling", C.c_uint8), ("ep", C.c_uint8),
                 ("flags", C.c_uint8), ("halfmoves", C.c_uint16), ("fullmoves", C.c_uint16),
                 ("rep_key", C.c_uint64)]
+
+
+# the same 80-byte record as a numpy dtype (batched test data)
+POS_DTYPE = np.dtype({
+    "names": ["bb", "turn", "castling", "ep", "flags", "halfmoves", "fullmoves", "rep_key"],
+    "formats": [("<u8", (8,)), "u1", "u1", "u1", "u1", "<u2", "<u2", "<u8"],
+    "offsets": [0, 64, 65, 66, 67, 68, 70, 72], "itemsize": 80})
 
 
 class AzNetDesc(C.Structure):
@@ -60,6 +69,9 @@ class AzTiming(C.Structure):
 # az_eval_fn (include/az.h): int (*)(void* ctx, const az_pos*, int n, float* policy, float* value)
 EVAL_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(AzPos), C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_float))
 
+# az_allreduce_fn (include/az.h): int (*)(void* ctx, float* buf, size_t n)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_float), C.c_size_t)
+
 # every symbol include/az.h declares: (name, restype, argtypes)
 P = C.POINTER
 SIGNATURES = [
@@ -96,6 +108,8 @@ SIGNATURES = [
     ("az_search_set_evaluator", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     ("az_search_set_roots", C.c_int, [C.c_void_p, P(C.c_int32), P(C.c_int32), P(C.c_int32), P(C.c_int32),
                                       C.c_int]),
+    ("az_search_set_roots_from", C.c_int, [C.c_void_p, P(AzPos), P(C.c_int32), P(C.c_int32), P(C.c_int32),
+                                           P(C.c_int32), C.c_int]),
     ("az_search_run", C.c_int, [C.c_void_p, P(C.c_float), P(C.c_uint32), P(C.c_int32)]),
     ("az_search_read_roots", C.c_int, [C.c_void_p, P(C.c_float), P(C.c_uint32), P(C.c_int32)]),
     ("az_search_advance", C.c_int, [C.c_void_p, P(C.c_int32), C.c_int, P(C.c_int32)]),
@@ -132,6 +146,9 @@ SIGNATURES = [
     ("az_replay_save", C.c_int, [C.c_void_p, C.c_char_p]),
     ("az_replay_load", C.c_int, [C.c_char_p, C.c_int, P(C.c_void_p)]),
     ("az_trainer_set_comm", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int]),
+    ("az_trainer_set_host_reducer", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int]),
+    ("az_rules_probe", C.c_int, [C.c_int, P(AzPos), P(C.c_int32), C.c_int, P(AzPos), P(C.c_int32), P(C.c_int32),
+                                 P(C.c_int32), P(C.c_int32), P(C.c_int32), P(C.c_int32), P(C.c_uint64), P(C.c_float)]),
 ]
 
 if not os.path.exists(LIB_PATH):

@@ -150,3 +150,46 @@ def to_tensor(position):
     t = np.zeros((1, 19, 8, 8), np.float32)
     L.check(L.lib.az_pos_encode(C.byref(position._p), L.fptr(t)))
     return t
+
+
+def positions_to_array(positions):
+    """a numpy az_pos array (L.POS_DTYPE) from Positions"""
+    out = np.zeros(len(positions), L.POS_DTYPE)
+    buf = out.view(np.uint8).reshape(len(positions), 80)
+    for i, p in enumerate(positions):
+        buf[i] = np.frombuffer(bytes(p._p), np.uint8)
+    return out
+
+
+def array_position(arr, i):
+    """Position i of a numpy az_pos array"""
+    return Position(L.AzPos.from_buffer_copy(arr[i:i + 1].tobytes()))
+
+
+def rules_probe(parents, actions, device=0):
+    """az_rules_probe (test hook): the device rules path on items (parent, action) -- action < 0
+    probes the parent itself.  parents: a numpy az_pos array (L.POS_DTYPE) or a list of Positions.
+    Returns a dict: child (az_pos array), moves [n,256] / nmoves [n] (leaf generator, duplicates
+    included), root_moves / root_n (the roots' generator), outcome, in_check, fen_key, planes
+    [n,19,8,8]."""
+    if not isinstance(parents, np.ndarray):
+        parents = positions_to_array(parents)
+    par = np.ascontiguousarray(parents, L.POS_DTYPE)
+    n = len(par)
+    act = np.ascontiguousarray(actions, np.int32)
+    assert len(act) == n
+    child = np.zeros(n, L.POS_DTYPE)
+    mv = np.zeros((n, L.MAX_MOVES), np.int32)
+    nm = np.zeros(n, np.int32)
+    rmv = np.zeros((n, L.MAX_MOVES), np.int32)
+    rn = np.zeros(n, np.int32)
+    oc = np.zeros(n, np.int32)
+    chk = np.zeros(n, np.int32)
+    fk = np.zeros(n, np.uint64)
+    planes = np.zeros((n, 19, 8, 8), np.float32)
+    pp = lambda a: a.ctypes.data_as(C.POINTER(L.AzPos))
+    L.check(L.lib.az_rules_probe(device, pp(par), L.i32ptr(act), n, pp(child), L.i32ptr(mv), L.i32ptr(nm),
+                                 L.i32ptr(rmv), L.i32ptr(rn), L.i32ptr(oc), L.i32ptr(chk), L.u64ptr(fk),
+                                 L.fptr(planes)))
+    return dict(child=child, moves=mv, nmoves=nm, root_moves=rmv, root_n=rn, outcome=oc, in_check=chk,
+                fen_key=fk, planes=planes)

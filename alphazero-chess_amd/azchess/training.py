@@ -52,11 +52,11 @@ class SelfPlay:
         self.games = games
 
     def reset(self):
-        L.check(L.lib.az_selfplay_reset(self.search._h))
+        self.search.check(L.lib.az_selfplay_reset(self.search._h))
 
     def step(self):
         fin, act = C.c_int(), C.c_int()
-        L.check(L.lib.az_selfplay_step(self.search._h, C.byref(fin), C.byref(act)))
+        self.search.check(L.lib.az_selfplay_step(self.search._h, C.byref(fin), C.byref(act)))
         return fin.value, act.value
 
     def run_sims(self, nsims):
@@ -64,7 +64,7 @@ class SelfPlay:
         completes, its action choice / play / re-root follow as in step().  Returns
         (finished, active, move_done); active is -1 while the move is in progress."""
         fin, act, done = C.c_int(), C.c_int(), C.c_int()
-        L.check(L.lib.az_selfplay_run_sims(self.search._h, int(nsims), C.byref(fin), C.byref(act), C.byref(done)))
+        self.search.check(L.lib.az_selfplay_run_sims(self.search._h, int(nsims), C.byref(fin), C.byref(act), C.byref(done)))
         return fin.value, act.value, bool(done.value)
 
     def drain(self):
@@ -204,6 +204,22 @@ class Trainer:
     def set_comm(self, unique_id, rank, world):
         buf = (C.c_char * 128).from_buffer_copy(unique_id)
         L.check(L.lib.az_trainer_set_comm(self._h, buf, int(rank), int(world)))
+
+    def set_host_reducer(self, reduce, rank, world):
+        """Data-parallel steps with the exchange done on the host: reduce(buf) must replace the
+        float32 array buf by its element-wise sum over the `world` ranks (in place).  An exception
+        inside it fails the step."""
+        def fn(_ctx, ptr, n):
+            try:
+                reduce(np.ctypeslib.as_array(ptr, shape=(n,)))
+                return 0
+            except BaseException:            # nothing may unwind through the C frames
+                import traceback
+                traceback.print_exc()
+                return 1
+        self._reduce_fn = L.ALLREDUCE_FN(fn)   # kept alive with the trainer
+        L.check(L.lib.az_trainer_set_host_reducer(self._h, C.cast(self._reduce_fn, C.c_void_p), None, int(rank),
+                                                  int(world)))
 
     def timing(self, reset=False):
         """(step_ms, allreduce_ms, steps): device time summed over the steps since the last reset."""

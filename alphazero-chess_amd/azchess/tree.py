@@ -32,11 +32,14 @@ def _eval_trampoline(evaluator):
             np.ctypeslib.as_array(pol, shape=(n * 4096,))[:] = np.asarray(p, np.float32).reshape(n * 4096)
             np.ctypeslib.as_array(val, shape=(n,))[:] = np.asarray(v, np.float32).reshape(n)
             return 0
-        except Exception:                       # an exception must not unwind through the C frames
-            import traceback
-            traceback.print_exc()
+        except BaseException as e:              # nothing may unwind through the C frames, not even
+            import traceback                    # KeyboardInterrupt / SystemExit (ctypes would swallow
+            traceback.print_exc()               # them and report success over stale staging rows)
+            if not isinstance(e, Exception):
+                pending[0] = e
             return 1
-    return L.EVAL_FN(fn)
+    pending = [None]
+    return L.EVAL_FN(fn), pending
 
 
 class BatchedSearch:
@@ -53,9 +56,9 @@ class BatchedSearch:
         L.check(L.lib.az_search_create(model._h if model is not None else None, C.byref(self.cfg), device,
                                        C.byref(h)))
         self._h = h
-        self._eval_fn = None
+        self._eval_fn, self._pending = None, [None]
         if evaluator is not None:
-            self._eval_fn = _eval_trampoline(evaluator)     # kept alive as long as the engine
+            self._eval_fn, self._pending = _eval_trampoline(evaluator)     # kept alive as long as the engine
             L.check(L.lib.az_search_set_evaluator(self._h, C.cast(self._eval_fn, C.c_void_p), None))
 
     def __del__(self):
@@ -64,8 +67,17 @@ class BatchedSearch:
         except Exception:
             pass
 
-    def set_roots(self, histories, apply_noise=False, game_ids=None, noise_plies=None):
-        """MCTree::new(eval(root), state, apply_noise) for each game; state = startpos + history."""
+    def check(self, rc):
+        """L.check for calls that may run the caller's evaluator: a KeyboardInterrupt / SystemExit
+        raised inside it is re-raised here, after the C call has returned its error."""
+        e, self._pending[0] = self._pending[0], None
+        if e is not None:
+            raise e
+        return L.check(rc)
+
+    def set_roots(self, histories, apply_noise=False, game_ids=None, noise_plies=None, start=None):
+        """MCTree::new(eval(root), state, apply_noise) for each game; state = start + history
+        (start: a list of G Positions, e.g. from FENs; None = the startpos)."""
         assert len(histories) == self.games
         off = np.zeros(self.games + 1, np.int32)
         for g, h in enumerate(histories):
@@ -73,15 +85,21 @@ class BatchedSearch:
         flat = np.ascontiguousarray(np.concatenate([np.asarray(h, np.int32) for h in histories] + [np.zeros(1, np.int32)]))
         gid = np.arange(self.games, dtype=np.int32) if game_ids is None else np.asarray(game_ids, np.int32)
         plies = (off[1:] - off[:-1]).astype(np.int32) if noise_plies is None else np.asarray(noise_plies, np.int32)
-        L.check(L.lib.az_search_set_roots(self._h, L.i32ptr(flat), L.i32ptr(off), L.i32ptr(gid), L.i32ptr(plies),
-                                          1 if apply_noise else 0))
+        st = None
+        if start is not None:
+            assert len(start) == self.games
+            st = (L.AzPos * self.games)()
+            for g, p in enumerate(start):
+                st[g] = p._p
+        self.check(L.lib.az_search_set_roots_from(self._h, st, L.i32ptr(flat), L.i32ptr(off), L.i32ptr(gid),
+                                               L.i32ptr(plies), 1 if apply_noise else 0))
 
     def run(self):
         """monte_carlo_tree_search for every game -> (improved [G,4096], visits [G,4096], depth [G])."""
         imp = np.zeros((self.games, 4096), np.float32)
         vis = np.zeros((self.games, 4096), np.uint32)
         dep = np.zeros(self.games, np.int32)
-        L.check(L.lib.az_search_run(self._h, L.fptr(imp), L.u32ptr(vis), L.i32ptr(dep)))
+        self.check(L.lib.az_search_run(self._h, L.fptr(imp), L.u32ptr(vis), L.i32ptr(dep)))
         return imp, vis, dep
 
     def read_roots(self):
@@ -96,7 +114,7 @@ class BatchedSearch:
     def advance(self, actions, apply_noise=True):
         a = np.ascontiguousarray(actions, np.int32)
         res = np.zeros(self.games, np.int32)
-        L.check(L.lib.az_search_advance(self._h, L.i32ptr(a), 1 if apply_noise else 0, L.i32ptr(res)))
+        self.check(L.lib.az_search_advance(self._h, L.i32ptr(a), 1 if apply_noise else 0, L.i32ptr(res)))
         return res
 
     @property

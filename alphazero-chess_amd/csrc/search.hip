@@ -5,7 +5,7 @@
 //             PUCT u = C*P*sqrt(Nt)/(1+N), q = N>0 ? W/N : 0 (tree.rs:117-132, same f32
 //             operation order, -ffp-contract=off), wave-reduce argmax taking the FIRST
 //             max in `moves` order (strict '>' in the reference);
-//   k_expand  (1 lane / game): index_to_move + play_move (chess.rs:36-63): legal move
+//   k_expand  (1 wavefront / game): index_to_move + play_move (chess.rs:36-63): legal move
 //             generation of the child (its edge list), outcome(), repetition count over
 //             the tree path + game history, 50-move / 200-fullmove draws; non-terminal
 //             leaves become a node and a network row (tree.rs:146-167, 209-237);
@@ -15,7 +15,7 @@
 //             (tree.rs:134-143, 197-206).
 // Outside the timed (event-bracketed) steps the three tree kernels run as ONE launch,
 // k_step: backup of step i-1, select and expand of step i, one wavefront per game (the
-// expansion on its lane 0), so a simulation step is two launches: k_step and the tower.
+// expansion wave-parallel), so a simulation step is two launches: k_step and the tower.
 // A move step (k_finish) computes the improved policy visits/sum (tree.rs:110-114),
 // chooses the action (argmax with the LAST max at fullmoves >= 15, else WeightedIndex
 // over f32 cumulative sums: training.rs:310-321), records the EpisodeStep, plays it and
@@ -78,15 +78,9 @@ __global__ void __launch_bounds__(64) k_cache_insert(Engine E, int step) {
 
 
 
-// AZ_EXPAND_GPW games per wavefront (lanes >= GPW idle): the per-lane expansion is serial,
-// branchy integer code, so fewer games per wave means less divergence and more CUs in use.
-// Row allocation and the counters are one atomic per wave (ballot + popcount), not per game.
-#ifndef AZ_EXPAND_GPW
-#define AZ_EXPAND_GPW 4    // measured (tools/tower_ab): C2 4 -> 5 % faster per move than 16, 1 -> 13 % slower; C3 flat
-#endif
+// one wavefront per game (expand_leaf_wave); the row allocation on lane 0
 __global__ void __launch_bounds__(64) k_expand(Engine E, int step) {
     const int lane = threadIdx.x;
-#if AZ_EXPAND_WAVE
     const int g = vgpr_index(blockIdx.x);
     int nid = -1;
     const int kind = expand_leaf_wave(E, g, lane, &nid);
@@ -102,27 +96,6 @@ __global__ void __launch_bounds__(64) k_expand(Engine E, int step) {
             atomicAdd(&E.ctr->cache_hits, 1ull);
         }
     }
-#else
-    const int g = lane < AZ_EXPAND_GPW ? blockIdx.x * AZ_EXPAND_GPW + lane : E.G;
-    int nid = -1;
-    const int kind = expand_leaf(E, g, &nid);
-    const unsigned long long mrow = __ballot(kind == X_ROW);
-    if (mrow) {
-        const int leader = __builtin_ctzll(mrow);
-        int base = 0;
-        if (lane == leader) base = atomicAdd(step_rows(E, step), __popcll(mrow));
-        base = __shfl(base, leader, 64);
-        if (kind == X_ROW) {
-            const int row = base + __popcll(mrow & ((1ull << lane) - 1ull));
-            E.row_game[row] = g;
-            E.row_node[row] = nid;
-            E.leaf_row[g] = row;
-        }
-    }
-    const unsigned long long mt = __ballot(kind == X_TERMINAL), mc = __ballot(kind == X_CACHED);
-    if (lane == 0 && mt) atomicAdd(&E.ctr->terminal, (unsigned long long)__popcll(mt));
-    if (lane == 0 && mc) atomicAdd(&E.ctr->cache_hits, (unsigned long long)__popcll(mc));
-#endif
 }
 
 
@@ -137,7 +110,7 @@ __global__ void __launch_bounds__(256) k_backup(Engine E, int step) {
 // ------------------------------------------------------------------ fused step
 // One launch per simulation step instead of three: backup of step `bstep` (the previous one,
 // or none when < 0), then select and expand of step `step`, one wavefront per game (the
-// expansion on lane 0).  A game's backup, select and expand touch only that game's tree, so
+// expansion wave-parallel).  A game's backup, select and expand touch only that game's tree, so
 // the wave needs no grid-wide order; the wave's own global stores (backup) are made visible
 // to its later loads (select) by a workgroup-scope fence.  Rows are allocated with one atomic
 // per workgroup (STEP_WPB games).  bstep's row counter is read and cleared by one thread;
@@ -169,11 +142,7 @@ __global__ void __launch_bounds__(STEP_WPB * 64) k_step(Engine E, int step, int 
         select_game(E, g, lane);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         ST_STAMP(2);
-#if AZ_EXPAND_WAVE
         kind = expand_leaf_wave(E, g, lane, &nid, step);
-#else
-        if (lane == 0) kind = expand_leaf(E, g, &nid);
-#endif
     }
     ST_STAMP(3);
     if (lane == 0) { s_kind[w] = kind; s_nid[w] = nid; }
@@ -643,7 +612,7 @@ int sim_step(az_search* s, int step, hipEvent_t* ev) {
     if (ev) (void)hipEventRecord(ev[0], st);
     k_select<<<(G * 64 + 255) / 256, 256, 0, st>>>(E);
     if (ev) (void)hipEventRecord(ev[1], st);
-    k_expand<<<AZ_EXPAND_WAVE ? G : (G + AZ_EXPAND_GPW - 1) / AZ_EXPAND_GPW, 64, 0, st>>>(E, step);
+    k_expand<<<G, 64, 0, st>>>(E, step);
     if (ev) (void)hipEventRecord(ev[2], st);
     int rc = eval_step(s, step, ev);
     if (rc) return rc;
@@ -779,13 +748,23 @@ int run_sims(az_search* s, int i0 = 0, int i1 = -1) {
     return 0;
 }
 
-int upload_histories(az_search* s, const int32_t* hist, const int32_t* off, const int32_t* game_id,
-                     const int32_t* noise_ply) {
+// game g's history: start[g] (startpos when start is NULL), then hist[off[g]..off[g+1]) played;
+// the root is the last position, the earlier ones are its repetition history (pos_count, chess.rs:16)
+int upload_histories(az_search* s, const az_pos* start, const int32_t* hist, const int32_t* off,
+                     const int32_t* game_id, const int32_t* noise_ply) {
     const int G = s->E.G;
     std::vector<azc::Pos> hp((size_t)G * HMAX);
     std::vector<int> hl(G), gids(G), plies(G), act(G, 1);
     for (int g = 0; g < G; g++) {
         azc::Pos p = azc::startpos();
+        if (start) {
+            p = *reinterpret_cast<const azc::Pos*>(start + g);
+            bool chk;
+            azc::finalize(p, &chk);          // flags / rep_key from the position itself
+            const uint64_t kings = p.bb[azc::KING];
+            if (__builtin_popcountll(kings & p.bb[azc::WHITE_BB]) != 1 || __builtin_popcountll(kings & p.bb[azc::BLACK_BB]) != 1)
+                return fail("root start position of game " + std::to_string(g) + " needs one king per side");
+        }
         std::vector<azc::Pos> H{p};
         const int b = off ? off[g] : 0, e = off ? off[g + 1] : 0;
         for (int i = b; i < e; i++) {
@@ -1013,9 +992,14 @@ int az_search_set_evaluator(az_search* s, az_eval_fn fn, void* ctx) {
 
 int az_search_set_roots(az_search* s, const int32_t* hist, const int32_t* off, const int32_t* game_id,
                         const int32_t* noise_ply, int apply_noise) {
+    return az_search_set_roots_from(s, nullptr, hist, off, game_id, noise_ply, apply_noise);
+}
+
+int az_search_set_roots_from(az_search* s, const az_pos* start, const int32_t* hist, const int32_t* off,
+                             const int32_t* game_id, const int32_t* noise_ply, int apply_noise) {
     if (!s) return fail("null search");
     AZ_HIP(hipSetDevice(s->device));
-    int rc = upload_histories(s, hist, off, game_id, noise_ply);
+    int rc = upload_histories(s, start, hist, off, game_id, noise_ply);
     if (rc) return rc;
     rc = setup_roots(s, apply_noise, false);
     s->roots_fresh = rc == 0;
@@ -1079,7 +1063,7 @@ int az_search_advance(az_search* s, const int32_t* actions, int apply_noise, int
 int az_selfplay_reset(az_search* s) {
     if (!s) return fail("null search");
     AZ_HIP(hipSetDevice(s->device));
-    int rc = upload_histories(s, nullptr, nullptr, nullptr, nullptr);
+    int rc = upload_histories(s, nullptr, nullptr, nullptr, nullptr, nullptr);
     if (rc) return rc;
     AZ_HIP(hipMemset(s->E.ctr, 0, sizeof(Counters)));
     AZ_HIP(hipMemset(s->E.g_sims, 0, (size_t)s->E.G * 8));

@@ -190,95 +190,12 @@ struct EdgeSink {
 
 enum { X_NONE = 0, X_ROW, X_TERMINAL, X_CACHED };
 
-// one game's expansion; returns what the leaf became (X_ROW: new node that needs a network
-// row, *nid_out = its id)
-__device__ __forceinline__ int expand_leaf(const Engine& E, int g, int* nid_out) {
-    if (g >= E.G || !E.active[g] || E.leaf_kind[g] != LEAF_EVAL) return X_NONE;
-    Node* nodes = game_nodes(E, g);
-    Edge* edges = game_edges(E, g);
-    azc::Pos* npos = game_npos(E, g);
-    const int parent = E.leaf_node[g], eabs = E.leaf_edge[g];
-    // every per-game word the expansion needs is loaded up front: issued together, and ahead
-    // of the edge stores below, behind which the compiler would otherwise order them
-    const int idx = edges[eabs].idx & azc::IDX_MASK;
-    const azc::Pos pp = npos[parent];
-    const int ebeg = E.edge_count[g];
-    const int nid = E.node_count[g];
-    const int pdepth = nodes[parent].depth;
-    const int maxd = E.max_depth[g];
-    const int hlen = E.hist_len[g];
-    const int plen = E.leaf_len[g];                           // select's root -> parent path
-    const int* pn = E.path_node + (size_t)g * E.PMAX;
-    azc::Pos c = azc::play_index(pp, idx);
-    EdgeSink sink{edges + ebeg, 0};
-    bool chk = false, lep = false;
-    const int n = azc::gen_legal(c, sink, &chk, &lep);
-    c.flags = lep ? 1 : 0;
-    c.rep_key = azc::rep_key_of(c);
-    int res = azc::outcome(c, n, chk);                       // chess.rs:43-50
-    if (res == azc::ONGOING) {                               // chess.rs:52-60
-        // positions d plies back (d even: same side to move), d <= halfmoves: first the tree
-        // path (pn[plen - d], independent loads instead of a parent-pointer chase), then history
-        int cnt = 0;
-        const int hm = c.halfmoves;
-        const int dt = hm < plen ? hm : plen;
-        for (int d2 = 2; d2 <= dt; d2 += 2)
-            if (azc::chess_eq(npos[pn[plen - d2]], c)) cnt++;
-        int d = plen + 1;
-        const azc::Pos* hist = E.hist + (size_t)g * HMAX;
-        for (int hi = hlen - 2; hi >= 0 && d <= hm; hi--, d++)
-            if (!(d & 1) && azc::chess_eq(hist[hi], c)) cnt++;
-        if (cnt + 1 >= azc::REPETITIONS || c.halfmoves >= azc::NUM_HALFMOVES || c.fullmoves >= azc::NUM_FULLMOVES)
-            res = azc::DRAW;
-    }
-    if (res != azc::ONGOING) {
-        edges[eabs].child = res == azc::DRAW ? CHILD_DRAW : CHILD_WIN;
-        E.leaf_kind[g] = res == azc::DRAW ? LEAF_DRAW : LEAF_WIN;
-        return X_TERMINAL;
-    }
-    if (nid >= E.NMAX || ebeg + n > E.EMAX) {                // cannot happen with NMAX = S + 2
-        E.leaf_kind[g] = LEAF_DRAW;
-        atomicAdd(&E.ctr->overflow, 1);
-        return X_NONE;
-    }
-    Node nn;
-    nn.edge_begin = (uint32_t)ebeg;
-    nn.nedges = (uint16_t)n;
-    nn.depth = (uint16_t)(pdepth + 1);
-    nn.nsum = 0;
-    nn.parent = parent;
-    nodes[nid] = nn;
-    npos[nid] = c;
-    E.node_count[g] = nid + 1;
-    E.edge_count[g] = ebeg + n;
-    E.child_hdr[(size_t)g * E.EMAX + eabs] = (uint32_t)ebeg << 8 | (uint32_t)n;
-    edges[eabs].child = nid;
-    if (nn.depth > maxd) E.max_depth[g] = nn.depth;
-    if (E.cache_mask >= 0) {                                 // FEN cache lookup (tree.rs:214-219)
-        const uint64_t key = azc::fen_key(c);
-        for (int i = 0; i < CACHE_PROBES; i++) {
-            const int sl = (int)((key + (uint64_t)i) & (uint64_t)E.cache_mask);
-            if (E.c_state[sl] != 2u || E.c_key[sl] != key || E.c_n[sl] != n || !same_fen(E.c_pos[sl], c)) continue;
-            const float* pri = E.c_pri + (size_t)sl * MAX_EDGES;
-            for (int e = 0; e < n; e++) edges[ebeg + e].P = pri[e];
-            E.cached_value[g] = E.c_value[sl];
-            E.leaf_kind[g] = LEAF_CACHED;
-            return X_CACHED;
-        }
-    }
-    *nid_out = nid;
-    return X_ROW;
-}
-
 // ------------------------------------------------------------------ wave-parallel expansion
-// The same expansion with the 64 lanes of a wavefront (one game per wave): the legal-move list
-// of the new leaf in shakmaty order (azc::gen_legal's order), generated by
-// square -- lane s owns square s (the from-square; the to-square for pawn pushes) -- with one
-// wave prefix sum per generation group giving every move its position; the repetition count
-// compares one earlier position per lane.  Every value a branch depends on is wave-uniform.
-#ifndef AZ_EXPAND_WAVE
-#define AZ_EXPAND_WAVE 1   // 0: the one-lane serial expansion (A/B)
-#endif
+// One game's expansion with the 64 lanes of a wavefront: the legal-move list of the new leaf in
+// shakmaty order (azc::gen_legal's order), generated by square -- lane s owns
+// square s (the from-square; the to-square for pawn pushes) -- with one wave prefix sum per
+// generation group giving every move its position; the repetition count compares one earlier
+// position per lane.  Every value a branch depends on is wave-uniform.
 // move_to_index (chess.rs:73-116, azc::move_index) as selects only: the lanes of a wave index
 // different moves at once, and the if-chain form diverges into up to 12 serial paths
 __device__ __forceinline__ int move_index_bf(int from, int to, int turn) {
@@ -446,6 +363,21 @@ __device__ __forceinline__ int gen_legal_wave(const azc::Pos& p, Edge* __restric
     return total;
 }
 
+// The rules part of an expansion, on the position the leaf's move led to (play_index, chess.rs:42):
+// its legal moves as edges at `out` (gen_legal_wave), the legal-ep flag and repetition key, and
+// outcome() (chess.rs:43-50).  Returns the outcome, *n = the edge count (distinct indices).  Shared
+// with the rules probe (rules_probe.hip, az_rules_probe), which tests exactly this on the device.
+template <int NW = GEN_WAVES>
+__device__ __forceinline__ int leaf_rules(azc::Pos& c, Edge* __restrict__ out, int lane, int* n,
+                                          unsigned long long* tr = nullptr, bool* in_check = nullptr) {
+    bool chk = false, lep = false;
+    *n = gen_legal_wave<NW>(c, out, lane, &chk, &lep, tr);
+    c.flags = lep ? 1 : 0;
+    c.rep_key = azc::rep_key_of(c);
+    if (in_check) *in_check = chk;
+    return azc::outcome(c, *n, chk);
+}
+
 template <int NW = GEN_WAVES>
 __device__ __forceinline__ int expand_leaf_wave(const Engine& E, int g, int lane, int* nid_out, int step = -1) {
     // g is wave-uniform, and a provably uniform index would turn the per-game loads below into
@@ -475,14 +407,11 @@ __device__ __forceinline__ int expand_leaf_wave(const Engine& E, int g, int lane
 #ifdef AZ_STEP_TRACE
     if (tr && lane == 0) tr[11] = __builtin_amdgcn_s_memtime();
 #endif
-    bool chk = false, lep = false;
-    const int n = gen_legal_wave<NW>(c, edges + ebeg, lane, &chk, &lep, tr);
+    int n;
+    int res = leaf_rules<NW>(c, edges + ebeg, lane, &n, tr);
 #ifdef AZ_STEP_TRACE
     if (step == AZ_STEP_TRACE && lane == 0) E.trace[(size_t)g * 16 + 5] = __builtin_amdgcn_s_memtime();
 #endif
-    c.flags = lep ? 1 : 0;
-    c.rep_key = azc::rep_key_of(c);
-    int res = azc::outcome(c, n, chk);
     if (res == azc::ONGOING) {
         // earlier positions d plies back, d even, d <= halfmoves: d <= plen on the tree path
         // (pn[plen - d]), beyond it in the game history -- one candidate per lane

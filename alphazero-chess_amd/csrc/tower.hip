@@ -1082,17 +1082,9 @@ __device__ __forceinline__ void tower32w_board(const float* __restrict__ planes,
     }
     for (int b = 0; b < ta.blocks; b++) {
         const unsigned wb3 = b + 1 < ta.blocks ? ta.wwbytes[2 * b + 2] : 0u;   // after the last conv: nothing (reads 0)
-#if defined(AZ_WINO_NOWEIGHTS)   // timing experiment only (wrong results): zero-record descriptors, no weight traffic
-        const __amdgpu_buffer_rsrc_t r1 = t32_rsrc(ta.ww[2 * b], 0), r2 = t32_rsrc(ta.ww[2 * b + 1], 0), r3 = t32_rsrc(ta.ww[0], 0);
-        (void)wb3;
-#elif defined(AZ_WINO_SAMEW)     // timing experiment only (wrong results): every conv streams conv 0's weights
-        const __amdgpu_buffer_rsrc_t r1 = t32_rsrc(ta.ww[0], ta.wwbytes[0]), r2 = r1, r3 = r1;
-        (void)wb3;
-#else
         const __amdgpu_buffer_rsrc_t r1 = t32_rsrc(ta.ww[2 * b], ta.wwbytes[2 * b]);
         const __amdgpu_buffer_rsrc_t r2 = t32_rsrc(ta.ww[2 * b + 1], ta.wwbytes[2 * b + 1]);
         const __amdgpu_buffer_rsrc_t r3 = t32_rsrc(b + 1 < ta.blocks ? ta.ww[2 * b + 2] : ta.ww[2 * b + 1], wb3);
-#endif
         // F = 256 / 64: each conv transforms the next conv's chunk 0 at its end (conv_wino; C3 A/B
         // -0.3 % against the tail transform alone)
         constexpr bool PRE = F == 256 || F == 64;

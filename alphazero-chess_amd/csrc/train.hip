@@ -840,8 +840,11 @@ struct Trainer {
     int slot = 0;                            // per-BN statistics stride (>= every BN's channels)
     float *tpol = nullptr, *tval = nullptr, *planes = nullptr, *loss = nullptr, *vpart = nullptr;
     float* hloss = nullptr;                  // pinned [Bmax][2]
-    // data parallel
+    // data parallel: RCCL communicator, or a host-side reducer (az_trainer_set_host_reducer)
     ncclComm_t comm = nullptr;
+    az_allreduce_fn host_reduce = nullptr;
+    void* host_ctx = nullptr;
+    std::vector<float> host_buf;
     int rank = 0, world = 1;
     uint32_t* stat_idx = nullptr; float* stat_buf = nullptr; int nstat = 0;
     std::vector<void*> allocs;
@@ -1130,6 +1133,19 @@ float powi_f32(float x, long long n) {   // Rust f32::powi (repeated squaring in
     return r;
 }
 
+// the all-reduce (sum) of n floats at d through the caller's host reducer: device -> host, the
+// reducer, host -> device, on the trainer stream
+int host_allreduce(Trainer* T, float* d, size_t n, const char* what) {
+    T->host_buf.resize(n);
+    AZ_HIP(hipMemcpyAsync(T->host_buf.data(), d, n * sizeof(float), hipMemcpyDeviceToHost, T->st));
+    AZ_HIP(hipStreamSynchronize(T->st));
+    if (T->host_reduce(T->host_ctx, T->host_buf.data(), n) != 0)
+        return fail(std::string("host reducer failed (") + what + ")");
+    AZ_HIP(hipMemcpyAsync(d, T->host_buf.data(), n * sizeof(float), hipMemcpyHostToDevice, T->st));
+    AZ_HIP(hipStreamSynchronize(T->st));
+    return 0;
+}
+
 int trainer_apply(Trainer* T, double lr) {
     AZ_HIP(hipSetDevice(T->device));
     hipStream_t st = T->st;
@@ -1137,6 +1153,8 @@ int trainer_apply(Trainer* T, double lr) {
     if (T->comm) {   // a 1-rank communicator sums over itself: the identity, through RCCL
         if (ncclAllReduce(T->g, T->g, T->np, ncclFloat, ncclSum, T->comm, st) != ncclSuccess)
             return fail("ncclAllReduce (gradients) failed");
+    } else if (T->host_reduce) {
+        if (host_allreduce(T, T->g, T->np, "gradients")) return -1;
     }
     AZ_HIP(hipEventRecord(T->ev[2], st));
     T->t++;
@@ -1144,10 +1162,14 @@ int trainer_apply(Trainer* T, double lr) {
     const float decay_mul = (float)(1.0 - lr * 1e-4);   // WEIGHT_DECAY, parameters.rs:25
     tr::adamw_kernel<<<grid_for(T->np), 256, 0, st>>>(T->p, T->g, T->m, T->v, T->mask, T->np, 1.0f / (float)T->world,
                                                        decay_mul, (float)lr, bc1, bc2);
-    if (T->comm) {   // average the BatchNorm running statistics over ranks
+    if (T->comm || T->host_reduce) {   // average the BatchNorm running statistics over ranks
         tr::stats_pack_kernel<<<grid_for(T->nstat), 256, 0, st>>>(T->p, T->stat_idx, T->nstat, T->stat_buf, 0, 1.0f);
-        if (ncclAllReduce(T->stat_buf, T->stat_buf, T->nstat, ncclFloat, ncclSum, T->comm, st) != ncclSuccess)
-            return fail("ncclAllReduce (running statistics) failed");
+        if (T->comm) {
+            if (ncclAllReduce(T->stat_buf, T->stat_buf, T->nstat, ncclFloat, ncclSum, T->comm, st) != ncclSuccess)
+                return fail("ncclAllReduce (running statistics) failed");
+        } else if (host_allreduce(T, T->stat_buf, (size_t)T->nstat, "running statistics")) {
+            return -1;
+        }
         tr::stats_pack_kernel<<<grid_for(T->nstat), 256, 0, st>>>(T->p, T->stat_idx, T->nstat, T->stat_buf, 1,
                                                                   1.0f / (float)T->world);
     }
@@ -1375,9 +1397,22 @@ int az_trainer_set_comm(az_trainer* t, const void* unique_id, int rank, int worl
     Trainer* T = t->t;
     AZ_HIP(hipSetDevice(T->device));
     if (T->comm) { ncclCommDestroy(T->comm); T->comm = nullptr; }
+    T->host_reduce = nullptr;
     ncclUniqueId id;
     memcpy(&id, unique_id, sizeof(id));
     if (ncclCommInitRank(&T->comm, world, id, rank) != ncclSuccess) return fail("ncclCommInitRank failed");
+    T->rank = rank;
+    T->world = world;
+    return 0;
+}
+
+int az_trainer_set_host_reducer(az_trainer* t, az_allreduce_fn fn, void* ctx, int rank, int world) {
+    if (!t || !fn || world < 1 || rank < 0 || rank >= world) return fail("az_trainer_set_host_reducer: bad arguments");
+    Trainer* T = t->t;
+    AZ_HIP(hipSetDevice(T->device));
+    if (T->comm) { ncclCommDestroy(T->comm); T->comm = nullptr; }
+    T->host_reduce = fn;
+    T->host_ctx = ctx;
     T->rank = rank;
     T->world = world;
     return 0;

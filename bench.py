@@ -61,22 +61,39 @@ def pmc_traffic(games, blocks, filters, dtype, winograd=True):
 
 
 def cpu_baseline(blocks, filters, threads, games, sims):
-    """Oracle (plain-C restatement of the reference, fp32) on the host cores: a bounded
-    sample of the same workload -- `games` searches of `sims` simulations each from the
-    start position with the same 20x256 net, one game per thread."""
+    """The reference's self-play on the host cores, a bounded sample of the same workload: `games`
+    games from the start position, one move of `sims` simulations each, same 20x256 net (seed 42).
+    Batched like the reference's batcher (training.rs:340-422): the oracle's trees (dense 4096
+    arrays, state clone per node, tree.rs) step in lockstep, OpenMP over games, and every
+    simulation step evaluates all pending leaves in ONE f32 forward through torch-CPU's oneDNN
+    convolutions (oracle/cpu_net.py: BN folded, channels-last, `threads` OpenMP threads).  Beside
+    it, the per-game port (one leaf at a time, naive C convolution) of earlier rounds."""
+    import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     import azchess as A
+    from cpu_net import CpuNet
     w = A.random_weights(blocks, filters, seed=42)
-    net = O.RefNet(blocks, filters, w)
-    cfg = O.make_cfg(sims=sims, noise=True, seed=42, eval_kind=1, net=net, threads=threads)
+    net = CpuNet(blocks, filters, w, threads=threads)
+    net.forward(np.zeros((games, 19, 8, 8), np.float32))          # warm oneDNN's kernels
+    cfg = O.make_cfg(sims=sims, noise=True, seed=42, eval_kind=1, threads=threads)
     t0 = time.perf_counter()
-    steps, nsims, nevals = O.selfplay(cfg, games, max_plies=1)
+    steps, nsims, nevals = O.selfplay_batched(cfg, games, max_plies=1, evaluator=net.forward)
     dt = time.perf_counter() - t0
-    return {"value": nsims / dt, "unit": "sims/s", "cores": threads, "kind": "port",
-            "sample": "%d games x 1 move x %d sims (+ shared root eval), %dx%d fp32 oracle, %d threads, %.1f s"
-                      % (games, sims, blocks, filters, threads, dt),
-            "evals": nevals}
+    out = {"value": nsims / dt, "unit": "sims/s", "cores": threads, "kind": "port",
+           "sample": "%d games x 1 move x %d sims (+ shared root eval) in lockstep, one batched f32 forward per "
+                     "simulation step (torch-CPU oneDNN, BN folded), %dx%d net, %d threads, %.1f s"
+                     % (games, sims, blocks, filters, threads, dt),
+           "evals": nevals}
+    rnet = O.RefNet(blocks, filters, w)
+    pcfg = O.make_cfg(sims=max(sims // 2, 1), noise=True, seed=42, eval_kind=1, net=rnet, threads=threads)
+    t0 = time.perf_counter()
+    _, psims, _ = O.selfplay(pcfg, 16, max_plies=1)
+    pdt = time.perf_counter() - t0
+    out["per_game_port"] = {"value": psims / pdt, "unit": "sims/s", "cores": threads,
+                            "sample": "16 games x 1 move x %d sims, one leaf per game at a time, naive C "
+                                      "convolution (oracle/net_ref.c), %.1f s" % (max(sims // 2, 1), pdt)}
+    return out
 
 
 def train_child(a):
@@ -363,14 +380,14 @@ def main():
                     help="FEN cache entries for an extra with_fen_cache leg (CACHE_CAPACITY = 500000; 0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu-games", type=int, default=16)
-    ap.add_argument("--cpu-sims", type=int, default=32, help="sims per sampled search (~12 s of host work at 20x256)")
+    ap.add_argument("--cpu-games", type=int, default=64)
+    ap.add_argument("--cpu-sims", type=int, default=32, help="sims per sampled search (batched leg ~10 s of host work at 20x256)")
     ap.add_argument("--train-steps", type=int, default=5, help="timed training steps (0 = skip the training phase)")
     ap.add_argument("--train-batch", type=int, default=512, help="positions per rank (BATCH_SIZE, parameters.rs:17)")
     ap.add_argument("--train-timeout", type=int, default=240)
     ap.add_argument("--games-leg", type=int, default=1,
                     help="1: also play C2's games (256 x 800 sims, 6x64 f32) from startpos to the end on every rank "
-                         "and report the measured games/hr (0 = skip)")
+                         "and report the measured games/hr (0 = skip); its wall time is in legs_wall_s")
     ap.add_argument("--same-device", action="store_true",
                     help="test only: every rank runs on device 0 and the RCCL training leg is skipped (exercises the "
                          "N>1 rank path with the real engine on a 1-GPU box; not a scaling measurement)")
@@ -543,8 +560,11 @@ def main():
 
     # headline: reference precision, no FEN cache -> every non-terminal simulation evaluates its
     # leaf on the network
+    legs = {}
+    tl = time.perf_counter()
     net = make_net(args.dtype)
     elapsed, tot, tm, sims_rank = phase(net, 0, args.steps, True)
+    legs["headline (incl. warmup, profile pass)"] = time.perf_counter() - tl
     roof = roofline(tm, args.dtype, net)
     del net
     sims_all, evals_all, term_all = tot["sims"], tot["evals"], tot["terminal"]
@@ -554,6 +574,7 @@ def main():
     bf16_res = None
     bf16_steps = args.steps if args.bf16_steps < 0 else args.bf16_steps
     if args.dtype == "f32" and bf16_steps > 0:
+        tl = time.perf_counter()
         net16 = make_net("bf16")
         e16, t16, tm16, _ = phase(net16, 0, bf16_steps, True)
         bf16_res = {"value": t16["sims"] / e16, "unit": "sims/s", "steps": bf16_steps,
@@ -563,6 +584,7 @@ def main():
                     "note": "bf16 weights/activations, f32 accumulate: narrower than the reference's f32, "
                             "reported beside the headline, not as it"}
         del net16
+        legs["bf16_mode"] = time.perf_counter() - tl
 
     # the reference's FEN cache (tree.rs:214-219) on the same window, on request
     cache_res = None
@@ -576,11 +598,15 @@ def main():
     # measured games/hr: C2's configuration played to the end on every rank (training.rs:294-378)
     games_leg = None
     if args.games_leg and not args.rehearse:
+        tl = time.perf_counter()
         games_leg = play_games_leg(A, local, sh["seed"], world, barrier, synchronize)
+        legs["games_per_hr_measured (C2 played to the end)"] = time.perf_counter() - tl
 
     training = None
     if args.train_steps > 0 and not args.rehearse and not args.same_device:
+        tl = time.perf_counter()
         training = train_phase(args, A, rank, world, local)
+        legs["training"] = time.perf_counter() - tl
     if rank != 0:
         dist.destroy_process_group()
         return
@@ -628,7 +654,9 @@ def main():
         "bf16_mode": bf16_res,
         "tree_walk": {"kernel": "k_select", "achieved_gbs": sel_gbs, "peak_gbs": PEAK_HBM_GBS,
                       "frac": sel_gbs / PEAK_HBM_GBS,
-                      "bytes_per_sim": tm["select_bytes"] / max(sims_rank, 1),
+                      # select_bytes counts every walk of the pass the events sample: the timed
+                      # window, or the profile pass after it (persistent kernel)
+                      "bytes_per_sim": tm["select_bytes"] / max(tm["profile_sim_steps"] * G, 1),
                       "avg_ms_per_launch": tm["select_ms"] / max(tm["select_launches"], 1)},
         "sim_step_ms": {k: tm[k + "_ms"] / max(tm["sim_steps"], 1)
                         for k in ("select", "expand", "encode", "tower", "heads", "backup")},
@@ -663,8 +691,12 @@ def main():
                     "of a separate run); the timed window (%d x %d simulation steps) is too short for games to "
                     "finish" % (gl["games"], args.steps, K)}
     if world == 1 and not args.no_cpu_baseline and not args.rehearse:
+        tl = time.perf_counter()
         out["cpu_baseline"] = cpu_baseline(args.blocks, args.filters, args.cpu_threads, args.cpu_games,
                                            args.cpu_sims)
+        legs["cpu_baseline"] = time.perf_counter() - tl
+    out["legs_wall_s"] = {k: round(v, 2) for k, v in legs.items()}
+    out["legs_note"] = "wall time of every leg this run executed (rank 0); only the headline's timed window is `value`"
     print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()

@@ -110,8 +110,11 @@ enum { AZ_EVAL_NET = 0, AZ_EVAL_SYNTHETIC = 1, AZ_EVAL_CALLBACK = 2 };
  * az_selfplay_* once per simulation step with the n leaf positions that need an evaluation (every
  * game's pending InferenceRequest of that step, in batch-row order).  It fills policy[n * 4096]
  * (AlphaZero::forward's softmax row, agent.rs:128-130: the engine reads it at the legal move
- * indices only) and value[n] (side-to-move view, tanh output).  Return 0 on success; a non-zero
- * return aborts the search call with an error.  Buffers are engine-owned and valid for the call. */
+ * indices only) and value[n] (side-to-move view, tanh output).  The rows must be what the
+ * reference's forward gives: finite, non-negative, a softmax over the 4096 entries -- the engine
+ * takes the legal entries as priors unchecked (PUCT of a NaN prior never wins a selection).
+ * Return 0 on success; a non-zero return aborts the search call with an error.  Buffers are
+ * engine-owned and valid for the call. */
 typedef int (*az_eval_fn)(void* ctx, const az_pos* positions, int n, float* policy, float* value);
 typedef struct {
     int games;          /* concurrent games G on this GPU (NUM_EPISODES, parameters.rs:13) */
@@ -146,6 +149,12 @@ int az_search_set_evaluator(az_search* s, az_eval_fn fn, void* ctx);
  * self-play move left in progress by az_selfplay_run_sims (its simulations are discarded). */
 int az_search_set_roots(az_search* s, const int32_t* hist, const int32_t* off, const int32_t* game_id,
                         const int32_t* noise_ply, int apply_noise);
+/* The same from arbitrary states, MCTree::new(policy, state, apply_noise) with any GameState
+ * (tree.rs:84-104): game g's state starts at start[g] (NULL = startpos for every game; its
+ * repetition multiset holds start[g] once) and plays hist[off[g]..off[g+1]) through play_move, so
+ * the root is the last position and every earlier one counts toward threefold (chess.rs:52-60). */
+int az_search_set_roots_from(az_search* s, const az_pos* start, const int32_t* hist, const int32_t* off,
+                             const int32_t* game_id, const int32_t* noise_ply, int apply_noise);
 /* monte_carlo_tree_search for every game (tree.rs:106-115 / 169-178).  Outputs (any may
  * be NULL): improved policy [G,4096], visits [G,4096], max_subtree_depth [G]. */
 int az_search_run(az_search* s, float* improved, uint32_t* visits, int32_t* depth);
@@ -266,6 +275,14 @@ int az_trainer_timing(az_trainer* t, double* step_ms, double* allreduce_ms, int6
  * size), every rank passes it to az_trainer_set_comm. */
 int az_comm_unique_id(void* out, int cap);
 int az_trainer_set_comm(az_trainer* t, const void* unique_id, int rank, int world);
+/* The same data-parallel step with the exchange done by the caller on the host (no RCCL: e.g.
+ * gloo / MPI between hosts, or a test driving two ranks in one process): at each apply, fn(ctx,
+ * buf, n) must replace buf[0..n) (host memory) by its element-wise sum over the `world` ranks --
+ * once for the gradients (before clipping; the AdamW step then scales by 1/world) and once for
+ * the BatchNorm running statistics (then scaled by 1/world).  Return 0 on success.  Replaces a
+ * communicator set by az_trainer_set_comm. */
+typedef int (*az_allreduce_fn)(void* ctx, float* buf, size_t n);
+int az_trainer_set_host_reducer(az_trainer* t, az_allreduce_fn fn, void* ctx, int rank, int world);
 
 /* ---- replay buffer: memory.rs ReplayBuffer, host memory ------------ */
 typedef struct az_replay az_replay;
@@ -284,6 +301,21 @@ int az_replay_sample(az_replay* r, int batch, uint64_t seed, float* planes, floa
 /* save / load (memory.rs:107-117): bincode 2 standard-config file of the reference's layout */
 int az_replay_save(const az_replay* r, const char* path);
 int az_replay_load(const char* path, int capacity, az_replay** out);
+
+/* ---- test hook: the device rules path (parity tests; the engine never calls it) ----------
+ * Runs, on the GPU, exactly what a leaf expansion runs (index_to_move + play, chess.rs:118-171 /
+ * 42; the wave-parallel legal move generator; outcome(), chess.rs:43-50; the legal-ep flag and
+ * repetition key) plus the roots' serial generator and the towers' plane staging (to_tensor,
+ * chess.rs:191-245), for n items: item i = parent[i] with action[i] played (action[i] < 0: parent[i]
+ * itself; an illegal action is refused on the host).  Outputs (child required, the rest may be NULL):
+ * child[n] (flags, rep_key set); moves[n][256] / nmoves[n]: the leaf generator's legal indices in
+ * shakmaty order with under-promotion duplicates (MCTree::new's `moves`, tree.rs:86-89);
+ * root_moves[n][256] / root_n[n]: the same from the roots' generator; outcome[n] (AZ_ONGOING /
+ * AZ_DRAW / AZ_WHITE_WINS / AZ_BLACK_WINS, no repetition); in_check[n]; fen_key[n] (the FEN-cache
+ * key, tree.rs:214); planes[n][19][64]. */
+int az_rules_probe(int device, const az_pos* parent, const int32_t* action, int n, az_pos* child, int32_t* moves,
+                   int32_t* nmoves, int32_t* root_moves, int32_t* root_n, int32_t* outcome, int32_t* in_check,
+                   uint64_t* fen_key, float* planes);
 
 #ifdef __cplusplus
 }

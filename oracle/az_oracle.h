@@ -79,6 +79,7 @@ typedef struct {
     int32_t* counts;
 } ref_game;
 void ref_game_new(ref_game* g);                           /* chess.rs:20-26 */
+void ref_game_from(ref_game* g, const ref_pos* start);      /* repetition multiset {start: 1} */
 void ref_game_clone(ref_game* dst, const ref_game* src);
 void ref_game_free(ref_game* g);
 int  ref_play_move(ref_game* g, ref_move m);              /* chess.rs:36-63 */
@@ -152,8 +153,29 @@ typedef struct {
 int ref_search_game(const ref_search_cfg* cfg, const ref_replay* rep, const int32_t* history, int nhist,
                     int noise, uint64_t noise_key, ref_search_out* out);
 
+/* The same from an arbitrary position: GameState{start, {start: 1}} + history (tree.rs:84-104). */
+int ref_search_from(const ref_search_cfg* cfg, const ref_replay* rep, const ref_pos* start, const int32_t* history,
+                    int nhist, int noise, uint64_t noise_key, ref_search_out* out);
+
+/* rules parity test data: packed positions, and the rules answers for (parent, index) items */
+void ref_pack(const ref_pos* p, int64_t n, uint64_t* bb, int32_t* meta);
+int64_t ref_rules_batch(const ref_pos* parent, const int32_t* action, int64_t n, ref_pos* child, int32_t* moves,
+                        int32_t* nmoves, int32_t* outcome, int32_t* in_check, int32_t* legal_ep, uint64_t* fen_key,
+                        float* planes);
+/* rules parity test data: uniform random playouts from the startpos, (parent, index) per ply */
+int64_t ref_random_playouts(uint64_t seed, int ngames, int max_plies, ref_pos* parents, int32_t* actions,
+                            int64_t cap);
+
 int64_t ref_selfplay(const ref_search_cfg* cfg, const ref_replay* rep, int ngames, int max_plies,
                      ref_step* steps, int64_t cap, int64_t* sims_done, int64_t* evals_done);
+
+/* The same self-play in lockstep with ONE batched evaluation per simulation step over every game's
+ * pending leaf (the reference's batcher, training.rs:369-422; the CPU baseline of SURVEY 8d):
+ * fn(ctx, planes [n][19][64] (to_tensor), n, policy [n][4096] out, value [n] out) -> 0 ok.
+ * fn == NULL: cfg->eval_kind per row.  Same records as ref_selfplay. */
+typedef int (*ref_eval_batch_fn)(void* ctx, const float* planes, int n, float* policy, float* value);
+int64_t ref_selfplay_batched(const ref_search_cfg* cfg, int ngames, int max_plies, ref_eval_batch_fn fn, void* ctx,
+                             ref_step* steps, int64_t cap, int64_t* sims_done, int64_t* evals_done);
 
 /* ---- arena / Elo (validation.rs:284-384, ratings.rs:113-144) ---- */
 int  ref_arena_choose(const float* policy, int fullmoves, int num_stochastic_moves, float u);

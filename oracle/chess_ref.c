@@ -553,6 +553,80 @@ void ref_game_new(ref_game* g) {
     g->n = 1;
 }
 
+/* a GameState whose repetition multiset starts at `start` (count 1), as GameState::new does
+ * for the startpos (chess.rs:20-26); for searches from an arbitrary MCTree::new state (tree.rs:84) */
+void ref_game_from(ref_game* g, const ref_pos* start) {
+    ref_game_new(g);
+    g->position = *start;
+    g->keys[0] = *start;
+}
+
+/* Uniform random playouts from the startpos for rules parity tests (test data, not a reference
+ * path): game k plays index_to_move(i) of a uniformly drawn legal index i (SplitMix64 of (seed,
+ * k, ply)) through play_move (chess.rs:36-63) until the result is not Ongoing or max_plies.
+ * Records every (parent position, index) pair; returns the count (<= cap). */
+int64_t ref_random_playouts(uint64_t seed, int ngames, int max_plies, ref_pos* parents, int32_t* actions,
+                            int64_t cap) {
+    int64_t n = 0;
+    for (int k = 0; k < ngames; k++) {
+        ref_game g;
+        ref_game_new(&g);
+        for (int ply = 0; ply < max_plies; ply++) {
+            int32_t idx[REF_MAX_MOVES];
+            int nl = ref_legal_indices(&g.position, idx);
+            if (nl == 0) break;
+            uint64_t r = ref_splitmix64(ref_splitmix64(seed ^ ((uint64_t)k << 20)) ^ (uint64_t)ply);
+            int a = idx[r % (uint64_t)nl];
+            if (n < cap) { parents[n] = g.position; actions[n] = a; }
+            n++;
+            ref_move m;
+            if (!ref_index_to_move(a, &g.position, &m)) break;
+            if (ref_play_move(&g, m) != REF_ONGOING) break;
+        }
+        ref_game_free(&g);
+    }
+    return n;
+}
+
+/* Packed view of positions for tests: bitboards P N B R Q K white black, and meta = {turn, castling,
+ * pseudo-legal ep (64 = none), halfmoves, fullmoves} -- the fields of the product's az_pos. */
+void ref_pack(const ref_pos* p, int64_t n, uint64_t* bb, int32_t* meta) {
+    for (int64_t i = 0; i < n; i++) {
+        ref_pos_bitboards(&p[i], bb + 8 * i);
+        int ep = ref_pseudo_legal_ep(&p[i]);
+        int32_t* m = meta + 5 * i;
+        m[0] = p[i].turn; m[1] = p[i].castling; m[2] = ep < 0 ? 64 : ep;
+        m[3] = p[i].halfmoves; m[4] = p[i].fullmoves;
+    }
+}
+
+/* The rules answers for n items (test data): child = parent with index_to_move(action) played
+ * (action < 0: the parent itself), its legal indices with duplicates (tree.rs:86-89), outcome(),
+ * in-check, legal ep square (-1 = none), FEN key and to_tensor planes.  Returns the number of
+ * items whose action was not legal (their outputs are the parent's). */
+int64_t ref_rules_batch(const ref_pos* parent, const int32_t* action, int64_t n, ref_pos* child, int32_t* moves,
+                        int32_t* nmoves, int32_t* outcome, int32_t* in_check, int32_t* legal_ep, uint64_t* fen_key,
+                        float* planes) {
+    int64_t bad = 0;
+#pragma omp parallel for schedule(dynamic, 256) reduction(+:bad)
+    for (int64_t i = 0; i < n; i++) {
+        ref_pos c = parent[i];
+        if (action[i] >= 0) {
+            ref_move m;
+            if (ref_index_to_move(action[i], &c, &m)) ref_play_unchecked(&c, m);
+            else bad++;
+        }
+        child[i] = c;
+        nmoves[i] = ref_legal_indices(&c, moves + (size_t)i * REF_MAX_MOVES);
+        outcome[i] = ref_outcome(&c);
+        in_check[i] = ref_in_check(&c);
+        legal_ep[i] = ref_legal_ep(&c);
+        fen_key[i] = ref_fen_key(&c);
+        ref_to_tensor(&c, planes + (size_t)i * 19 * 64);
+    }
+    return bad;
+}
+
 void ref_game_clone(ref_game* dst, const ref_game* src) {
     memset(dst, 0, sizeof(*dst));
     dst->position = src->position;

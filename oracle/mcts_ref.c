@@ -270,8 +270,14 @@ static mct* mct_traverse_new(mct* t, int action, const ref_search_cfg* cfg, int 
 
 int ref_search_game(const ref_search_cfg* cfg, const ref_replay* rep, const int32_t* history, int nhist,
                     int noise, uint64_t noise_key, ref_search_out* out) {
+    return ref_search_from(cfg, rep, NULL, history, nhist, noise, noise_key, out);
+}
+
+int ref_search_from(const ref_search_cfg* cfg, const ref_replay* rep, const ref_pos* start, const int32_t* history,
+                    int nhist, int noise, uint64_t noise_key, ref_search_out* out) {
     ref_game g;
-    ref_game_new(&g);
+    if (start) ref_game_from(&g, start);
+    else ref_game_new(&g);
     for (int i = 0; i < nhist; i++) {
         ref_move m;
         if (!ref_index_to_move(history[i], &g.position, &m)) { ref_game_free(&g); return -1; }
@@ -459,4 +465,216 @@ void ref_compute_elos(const float* wm, int n, float base_elo, float* elos) {
             elos[i] += 8.0f * (actual - expected);
         }
     }
+}
+
+/* ---------------- batched lockstep self-play (CPU baseline) ----------------
+ * The reference's self-play structure on the host -- one task per game, each with ONE outstanding
+ * leaf, a batcher running one forward over every pending request (training.rs:340-422) -- in
+ * lockstep: per simulation step every game selects its leaf (tree.rs:117-132, same dense-4096
+ * trees as above, OpenMP over games), the leaves that need the network go through ONE batched
+ * evaluation (to_tensor planes in, softmax rows + values out: process_batch), then every game
+ * inserts its child and backs up (tree.rs:134-143).  A game's simulations stay sequential, so
+ * its results equal run_episode's bit for bit given the same evaluations (tests/
+ * test_oracle_rules_data.py).  fn == NULL evaluates through cfg->eval_kind instead. */
+typedef struct {
+    mct** node;
+    int32_t* idx;
+    int len;
+    ref_game leaf;
+    int kind;              /* 0 needs the network, 1 draw, 2 the mover won */
+    int row;
+} pend_leaf;
+
+static void batched_select(mct* t, const ref_search_cfg* cfg, pend_leaf* p) {
+    p->len = 0;
+    for (;;) {
+        float max_value = -INFINITY, total_visits = 0.0f;
+        int max_index = 0;
+        for (int i = 0; i < REF_ACTION_SPACE; i++) total_visits += t->visits[i];
+        total_visits = total_visits + 1.0f;                            /* tree.rs:121 */
+        for (int k = 0; k < t->nmoves; k++) {                          /* tree.rs:123-132 */
+            int i = t->moves[k];
+            float u_value = cfg->c_puct * t->policy[i] * sqrtf(total_visits) / (1.0f + t->visits[i]);
+            float q_value = t->visits[i] > 0.0f ? t->scores[i] / t->visits[i] : 0.0f;
+            float value = q_value + u_value;
+            if (value > max_value) { max_value = value; max_index = i; }
+        }
+        p->node[p->len] = t;
+        p->idx[p->len] = max_index;
+        p->len++;
+        mct* c = mct_find(t, max_index);
+        if (c) { t = c; continue; }
+        ref_game_clone(&p->leaf, &t->state);                           /* tree.rs:210-212 */
+        ref_move m;
+        if (!ref_index_to_move(max_index, &p->leaf.position, &m)) { fprintf(stderr, "oracle: Illegal move!\n"); abort(); }
+        int r = ref_play_move(&p->leaf, m);
+        p->kind = r == REF_ONGOING ? 0 : (r == REF_DRAW ? 1 : 2);
+        return;
+    }
+}
+
+static void batched_finish(pend_leaf* p, const ref_search_cfg* cfg, const float* policy, float nn_value) {
+    float v;                                                           /* the leaf's value, its mover's view */
+    mct* last = p->node[p->len - 1];
+    if (p->kind == 0) {
+        mct_insert(last, p->idx[p->len - 1], mct_new(cfg, policy, &p->leaf, 0, 0));
+        v = nn_value;
+    } else {
+        v = p->kind == 1 ? 0.0f : -1.0f;                               /* tree.rs:233-234 */
+    }
+    ref_game_free(&p->leaf);
+    float value = -v;                                                  /* value = -child value per level */
+    for (int l = p->len - 1; l >= 0; l--) {
+        p->node[l]->scores[p->idx[l]] += value;
+        p->node[l]->visits[p->idx[l]] += 1.0f;
+        value = -value;
+    }
+}
+
+typedef struct {
+    ref_game state;
+    mct* tree;
+    int ply, active, nh, result_code;
+    float scale;
+    step_tmp* hist;
+} batched_game;
+
+int64_t ref_selfplay_batched(const ref_search_cfg* cfg, int ngames, int max_plies, ref_eval_batch_fn fn, void* ctx,
+                             ref_step* steps, int64_t cap, int64_t* sims_done, int64_t* evals_done) {
+    const int S = cfg->sims, threads = cfg->threads > 0 ? cfg->threads : 1;
+    const int maxp = max_plies > 0 ? max_plies : 512;
+    eval_ctx ectx = {cfg, NULL, 0, 0};
+    float* pol = (float*)malloc(sizeof(float) * REF_ACTION_SPACE * (size_t)(ngames > 0 ? ngames : 1));
+    float* val = (float*)malloc(sizeof(float) * (size_t)(ngames > 0 ? ngames : 1));
+    float* planes = (float*)malloc(sizeof(float) * 19 * 64 * (size_t)(ngames > 0 ? ngames : 1));
+    int* rows = (int*)malloc(sizeof(int) * (size_t)(ngames > 0 ? ngames : 1));
+    int64_t total_sims = 0, total_evals = 0;
+    int failed = 0;
+    /* shared root evaluation of the start position (training.rs:344-350) */
+    batched_game* gm = (batched_game*)calloc((size_t)ngames, sizeof(batched_game));
+    ref_game g0;
+    ref_game_new(&g0);
+    if (fn) {
+        ref_to_tensor(&g0.position, planes);
+        failed |= fn(ctx, planes, 1, pol, val) != 0;
+    } else {
+        evaluate(&ectx, &g0.position, pol, val);
+    }
+    total_evals++;
+    ref_game_free(&g0);
+    for (int g = 0; g < ngames; g++) {
+        ref_game_new(&gm[g].state);
+        gm[g].tree = mct_new(cfg, pol, &gm[g].state, cfg->noise, ref_stream_key(cfg->seed, (uint64_t)g, 0, 0));
+        gm[g].active = 1;
+        gm[g].hist = (step_tmp*)malloc(sizeof(step_tmp) * (size_t)maxp);
+    }
+    pend_leaf* pl = (pend_leaf*)calloc((size_t)ngames, sizeof(pend_leaf));
+    for (int g = 0; g < ngames; g++) {
+        pl[g].node = (mct**)malloc(sizeof(mct*) * (size_t)(S + 2));
+        pl[g].idx = (int32_t*)malloc(sizeof(int32_t) * (size_t)(S + 2));
+    }
+    ref_search_out* so = (ref_search_out*)malloc(sizeof(ref_search_out) * (size_t)(ngames > 0 ? ngames : 1));
+    for (;;) {
+        int live = 0;
+        for (int g = 0; g < ngames; g++) live += gm[g].active;
+        if (!live) break;
+        for (int s = 0; s < S && !failed; s++) {
+#pragma omp parallel for schedule(dynamic, 4) num_threads(threads)
+            for (int g = 0; g < ngames; g++)
+                if (gm[g].active) batched_select(gm[g].tree, cfg, &pl[g]);
+            int n = 0;                                                 /* the batcher's requests */
+            for (int g = 0; g < ngames; g++)
+                if (gm[g].active && pl[g].kind == 0) { pl[g].row = n; rows[n++] = g; }
+            if (n) {
+                if (fn) {
+#pragma omp parallel for num_threads(threads)
+                    for (int r = 0; r < n; r++) ref_to_tensor(&pl[rows[r]].leaf.position, planes + (size_t)r * 19 * 64);
+                    failed |= fn(ctx, planes, n, pol, val) != 0;       /* process_batch: one forward */
+                } else {
+#pragma omp parallel for schedule(dynamic, 1) num_threads(threads)
+                    for (int r = 0; r < n; r++) {
+                        eval_ctx c = {cfg, NULL, 0, 0};
+                        evaluate(&c, &pl[rows[r]].leaf.position, pol + (size_t)r * REF_ACTION_SPACE, val + r);
+                    }
+                }
+                total_evals += n;
+            }
+#pragma omp parallel for schedule(dynamic, 4) num_threads(threads)
+            for (int g = 0; g < ngames; g++) {
+                if (!gm[g].active) continue;
+                const int r = pl[g].kind == 0 ? pl[g].row : 0;
+                batched_finish(&pl[g], cfg, pol + (size_t)r * REF_ACTION_SPACE, pl[g].kind == 0 ? val[r] : 0.0f);
+            }
+            total_sims += live;
+        }
+        if (failed) break;
+        /* per move: improved policy, record, action choice, play, re-root (run_episode, training.rs:294-338) */
+#pragma omp parallel for schedule(dynamic, 1) num_threads(threads)
+        for (int g = 0; g < ngames; g++) {
+            batched_game* G = &gm[g];
+            if (!G->active) continue;
+            mct* t = G->tree;
+            float sum = 0.0f;
+            for (int i = 0; i < REF_ACTION_SPACE; i++) sum += t->visits[i];
+            for (int i = 0; i < REF_ACTION_SPACE; i++) { so[g].visits[i] = t->visits[i]; so[g].improved[i] = t->visits[i] / sum; }
+            so[g].depth = mct_depth(t);
+            float turn = G->state.position.turn == 0 ? 1.0f : -1.0f;
+            step_tmp* st = &G->hist[G->nh++];
+            st->ply = G->ply; st->depth = so[g].depth; st->turn = turn; st->key = ref_fen_key(&G->state.position);
+            st->nvis = 0;
+            for (int i = 0; i < REF_ACTION_SPACE; i++)
+                if (so[g].visits[i] != 0.0f && st->nvis < 256) { st->vis_idx[st->nvis] = i; st->vis_n[st->nvis] = so[g].visits[i]; st->nvis++; }
+            int action;
+            if ((uint32_t)G->state.position.fullmoves >= (uint32_t)cfg->temp_moves) {
+                action = argmax_last(so[g].improved);
+            } else {
+                uint64_t c = 0;
+                float u = ref_uniform01(ref_stream_key(cfg->seed, (uint64_t)g, (uint64_t)G->ply, 1), &c);
+                action = weighted_index(so[g].improved, u);
+            }
+            st->action = action;
+            ref_move m;
+            if (!ref_index_to_move(action, &G->state.position, &m)) { fprintf(stderr, "oracle: model played illegal move\n"); abort(); }
+            int r = ref_play_move(&G->state, m);
+            G->ply++;
+            if (r == REF_ONGOING && !(max_plies > 0 && G->ply >= max_plies)) {
+                G->tree = mct_traverse_new(G->tree, action, cfg, cfg->noise,
+                                           ref_stream_key(cfg->seed, (uint64_t)g, (uint64_t)G->ply, 0));
+                continue;
+            }
+            float result = 0.0f;
+            if (r == REF_ONGOING) G->result_code = -2;
+            else if (r == REF_DRAW) G->result_code = REF_DRAW;
+            else { result = turn; G->result_code = r; }
+            float decay = 1.0f - ((float)G->state.position.fullmoves / (2.0f * (float)REF_NUM_FULLMOVES));
+            G->scale = G->result_code == -2 ? 0.0f : result * decay;
+            for (int i = 0; i < G->nh; i++) G->hist[i].result = G->result_code;
+            mct_free(G->tree);
+            G->tree = NULL;
+            G->active = 0;
+        }
+    }
+    int64_t n = 0;
+    for (int g = 0; g < ngames; g++) {
+        for (int i = 0; i < gm[g].nh; i++) {
+            if (n < cap && steps) {
+                step_tmp* st = &gm[g].hist[i];
+                ref_step* o = &steps[n];
+                o->game = g; o->ply = st->ply; o->action = st->action; o->depth = st->depth;
+                o->final_value = st->turn * gm[g].scale;
+                o->result = st->result; o->fen_key = st->key; o->nvis = st->nvis;
+                memcpy(o->vis_idx, st->vis_idx, sizeof(o->vis_idx));
+                memcpy(o->vis_n, st->vis_n, sizeof(o->vis_n));
+            }
+            n++;
+        }
+        if (gm[g].tree) mct_free(gm[g].tree);
+        ref_game_free(&gm[g].state);
+        free(gm[g].hist);
+        free(pl[g].node); free(pl[g].idx);
+    }
+    free(gm); free(pl); free(so); free(pol); free(val); free(planes); free(rows);
+    if (sims_done) *sims_done = total_sims;
+    if (evals_done) *evals_done = total_evals;
+    return failed ? -1 : n;
 }

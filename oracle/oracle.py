@@ -105,6 +105,19 @@ def lib():
         L.ref_replay_free.argtypes = [C.c_void_p]
         L.ref_search_game.argtypes = [P(RefSearchCfg), C.c_void_p, P(C.c_int32), C.c_int, C.c_int, C.c_uint64,
                                       P(RefSearchOut)]
+        L.ref_search_from.argtypes = [P(RefSearchCfg), C.c_void_p, P(RefPos), P(C.c_int32), C.c_int, C.c_int,
+                                      C.c_uint64, P(RefSearchOut)]
+        L.ref_random_playouts.argtypes = [C.c_uint64, C.c_int, C.c_int, P(RefPos), P(C.c_int32), C.c_int64]
+        L.ref_random_playouts.restype = C.c_int64
+        L.ref_chess_eq.argtypes = [P(RefPos), P(RefPos)]
+        L.ref_pack.argtypes = [P(RefPos), C.c_int64, P(C.c_uint64), P(C.c_int32)]
+        L.ref_rules_batch.argtypes = [P(RefPos), P(C.c_int32), C.c_int64, P(RefPos), P(C.c_int32), P(C.c_int32),
+                                      P(C.c_int32), P(C.c_int32), P(C.c_int32), P(C.c_uint64), P(C.c_float)]
+        L.ref_rules_batch.restype = C.c_int64
+        L.ref_in_check.restype = C.c_int
+        L.ref_selfplay_batched.argtypes = [P(RefSearchCfg), C.c_int, C.c_int, C.c_void_p, C.c_void_p, P(RefStep),
+                                           C.c_int64, P(C.c_int64), P(C.c_int64)]
+        L.ref_selfplay_batched.restype = C.c_int64
         L.ref_selfplay.argtypes = [P(RefSearchCfg), C.c_void_p, C.c_int, C.c_int, P(RefStep), C.c_int64,
                                    P(C.c_int64), P(C.c_int64)]
         L.ref_selfplay.restype = C.c_int64
@@ -200,6 +213,27 @@ def outcome(p):
     return lib().ref_outcome(C.byref(p))
 
 
+def in_check(p):
+    return lib().ref_in_check(C.byref(p))
+
+
+def legal_ep(p):
+    return lib().ref_legal_ep(C.byref(p))
+
+
+def chess_eq(a, b):
+    return lib().ref_chess_eq(C.byref(a), C.byref(b))
+
+
+def random_playouts(seed, ngames, max_plies=400, cap=200000):
+    """(parents [n] RefPos array, actions [n]) of uniform random playouts (rules parity data)."""
+    parents = (RefPos * cap)()
+    actions = np.zeros(cap, np.int32)
+    n = lib().ref_random_playouts(seed, ngames, max_plies, parents, _i32p(actions), cap)
+    n = min(n, cap)
+    return parents[:n], actions[:n]
+
+
 class Game:
     """GameState restatement (chess.rs:13-63)."""
 
@@ -290,11 +324,13 @@ class Replay:
             pass
 
 
-def search_game(cfg, history=(), noise=False, noise_key=0, replay=None):
+def search_game(cfg, history=(), noise=False, noise_key=0, replay=None, start=None):
+    """MCTree::new(eval(root), state, noise) + monte_carlo_tree_search; state = GameState from
+    `start` (a RefPos; None = startpos) with `history` (move indices) played through play_move."""
     h = np.ascontiguousarray(history, np.int32)
     out = RefSearchOut()
-    rc = lib().ref_search_game(C.byref(cfg), replay._h if replay else None, _i32p(h), len(h), 1 if noise else 0,
-                               noise_key, C.byref(out))
+    rc = lib().ref_search_from(C.byref(cfg), replay._h if replay else None, C.byref(start) if start is not None else None,
+                               _i32p(h), len(h), 1 if noise else 0, noise_key, C.byref(out))
     if rc != 0:
         raise RuntimeError("ref_search_game failed: %d" % rc)
     return (np.frombuffer(out.visits, np.float32).copy(), np.frombuffer(out.improved, np.float32).copy(),
@@ -309,6 +345,41 @@ def selfplay(cfg, ngames, max_plies=0, replay=None, cap=100000):
                            C.byref(sims), C.byref(evals))
     if n < 0:
         raise RuntimeError("ref_selfplay: replay lookup failed")
+    out = []
+    for s in steps[:min(n, cap)]:
+        out.append(dict(game=s.game, ply=s.ply, action=s.action, depth=s.depth, final_value=s.final_value,
+                        result=s.result, fen_key=s.fen_key,
+                        visits={int(s.vis_idx[i]): float(s.vis_n[i]) for i in range(s.nvis)}))
+    return out, sims.value, evals.value
+
+
+EVAL_BATCH_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_float),
+                            C.POINTER(C.c_float))
+
+
+def selfplay_batched(cfg, ngames, max_plies=0, evaluator=None, cap=100000):
+    """ref_selfplay_batched: lockstep self-play with one batched evaluation per simulation step.
+    evaluator(planes [n,19,8,8] float32) -> (policy [n,4096], value [n]); None = cfg.eval_kind."""
+    steps = (RefStep * cap)()
+    sims, evals = C.c_int64(), C.c_int64()
+    fn = None
+    if evaluator is not None:
+        def cb(_ctx, planes, n, pol, val):
+            try:
+                x = np.ctypeslib.as_array(planes, shape=(n * 19 * 64,)).reshape(n, 19, 8, 8)
+                p, v = evaluator(x)
+                np.ctypeslib.as_array(pol, shape=(n * 4096,))[:] = np.asarray(p, np.float32).reshape(-1)
+                np.ctypeslib.as_array(val, shape=(n,))[:] = np.asarray(v, np.float32).reshape(-1)
+                return 0
+            except BaseException:
+                import traceback
+                traceback.print_exc()
+                return 1
+        fn = EVAL_BATCH_FN(cb)
+    n = lib().ref_selfplay_batched(C.byref(cfg), ngames, max_plies, C.cast(fn, C.c_void_p) if fn else None, None,
+                                   steps, cap, C.byref(sims), C.byref(evals))
+    if n < 0:
+        raise RuntimeError("ref_selfplay_batched: evaluation failed")
     out = []
     for s in steps[:min(n, cap)]:
         out.append(dict(game=s.game, ply=s.ply, action=s.action, depth=s.depth, final_value=s.final_value,
@@ -337,4 +408,57 @@ def compute_elos(winrate_matrix, base_elo):
     n = len(wm)
     out = np.zeros(n, np.float32)
     lib().ref_compute_elos(_fp(wm), n, C.c_float(base_elo), _fp(out))
+    return out
+
+
+# ------------------------------------------------------------------ batched rules data (tests)
+def as_pos_array(positions):
+    """a ctypes RefPos array from a sequence of RefPos (or an array already)."""
+    if isinstance(positions, C.Array):
+        return positions
+    arr = (RefPos * max(len(positions), 1))()
+    for i, p in enumerate(positions):
+        arr[i] = p
+    return arr
+
+
+def pack(positions, n=None):
+    """(bb [n,8] uint64, meta [n,5] int32: turn, castling, pseudo-legal ep (64 none), halfmoves,
+    fullmoves) of positions -- the fields the product's az_pos holds."""
+    arr = as_pos_array(positions)
+    n = len(positions) if n is None else n
+    bb = np.zeros((n, 8), np.uint64)
+    meta = np.zeros((n, 5), np.int32)
+    lib().ref_pack(arr, n, _u64p(bb), _i32p(meta))
+    return bb, meta
+
+
+def rules_batch(parents, actions):
+    """The oracle's answers for items (parent, action): dict of child (RefPos array), moves (list),
+    outcome, in_check, legal_ep, fen_key, planes [n,19,8,8]."""
+    n = len(actions)
+    arr = as_pos_array(parents)
+    act = np.ascontiguousarray(actions, np.int32)
+    child = (RefPos * max(n, 1))()
+    mv = np.zeros((n, 256), np.int32)
+    nm = np.zeros(n, np.int32)
+    oc = np.zeros(n, np.int32)
+    chk = np.zeros(n, np.int32)
+    lep = np.zeros(n, np.int32)
+    fk = np.zeros(n, np.uint64)
+    planes = np.zeros((n, 19, 8, 8), np.float32)
+    bad = lib().ref_rules_batch(arr, _i32p(act), n, child, _i32p(mv), _i32p(nm), _i32p(oc), _i32p(chk), _i32p(lep),
+                                _u64p(fk), _fp(planes))
+    if bad:
+        raise ValueError("%d illegal actions" % bad)
+    return dict(child=child, n=n, moves=mv, nmoves=nm, outcome=oc, in_check=chk, legal_ep=lep, fen_key=fk,
+                planes=planes)
+
+
+def take(positions, idx):
+    """RefPos array of positions[idx] (idx: integer array)."""
+    arr = as_pos_array(positions)
+    raw = np.frombuffer(arr, np.uint8).reshape(len(arr), C.sizeof(RefPos))[np.asarray(idx, np.int64)]
+    out = (RefPos * max(len(raw), 1))()
+    C.memmove(out, raw.tobytes(), raw.size)
     return out

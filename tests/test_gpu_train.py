@@ -234,3 +234,85 @@ def test_winograd_training_convs_match_direct(require_gpu, monkeypatch):
         cnt = 2 * shape[1] if bn else int(np.prod(shape))
         r = g0[o:o + cnt]
         assert np.linalg.norm(g1[o:o + cnt] - r) <= 1e-2 * max(np.linalg.norm(r), 1e-30), name
+
+
+def test_winograd_weight_grad_multi_split(require_gpu):
+    """the production Winograd weight grad (wino_wgrad_gemm_kernel, 512 rows of
+    (board, tile) per split, the splits summed by reduce_kernel) with more than one split: 80 boards
+    = 1280 rows = 3 splits, the last one partial.  Every gradient tensor against the float64 oracle
+    under the GPU's ReLU masks (1e-4 relative norm), at F = 256 where that kernel runs."""
+    blocks, filters, n = 2, 256, 80
+    w = A.random_weights(blocks, filters, seed=13)
+    planes, tpol, tval = batch(n, seed=81)
+    tr = A.Trainer(blocks, filters, weights=w, max_batch=n)
+    tr.compute_gradients(planes, tpol, tval)
+    g = tr.grads()
+    rg, _ = T.TrainRef(blocks, filters, w).grads(planes, tpol, tval, tr.relu_masks(n))
+    seg, _ = T.segments(blocks, filters)
+    zero_bias = bn_fed_biases(blocks)
+    checked = 0
+    for name, (o, shape, bn) in seg.items():
+        size = int(np.prod(shape))
+        parts = [(name + ".gamma", o, shape[1]), (name + ".beta", o + shape[1], shape[1])] if bn else [(name, o, size)]
+        for pname, off, cnt in parts:
+            if pname in zero_bias:
+                continue
+            a, r = g[off:off + cnt].astype(np.float64), rg[off:off + cnt]
+            err = np.linalg.norm(a - r) / max(np.linalg.norm(r), 1e-30)
+            assert err <= 1e-4, (pname, err)
+            checked += "res_blocks" in pname and pname.endswith("weight")
+    assert checked == 2 * blocks
+
+
+def test_data_parallel_world2_bit_exact(require_gpu):
+    """The world > 1 arithmetic of the data-parallel step (training.rs:137-200 sharded over ranks)
+    without a second GPU: two trainers on the two halves of a batch, their gradients summed by a
+    host reducer (az_trainer_set_host_reducer: the all-reduce RCCL would do, sum of two operands =
+    the same float32 sum in either order), then AdamW with world = 2 (gradient scale 1/2 before the
+    clip) and the BatchNorm running statistics averaged.  Both ranks end bit-identical, and equal
+    to the float32 restatement T.adamw_step(p, g0 + g1, ..., world=2) with averaged statistics.
+    Note the reference trains one batch of 512 on one device (training.rs:138): with 512 per rank
+    the global batch is 512 x world and BatchNorm sees per-rank statistics."""
+    import threading
+    blocks, filters, n = 2, 64, 16
+    w = A.random_weights(blocks, filters, seed=21)
+    planes, tpol, tval = batch(2 * n, seed=22)
+    ranks = [A.Trainer(blocks, filters, weights=w, max_batch=n) for _ in range(2)]
+    slots, bar = [None, None], threading.Barrier(2)
+
+    def reducer(rank):
+        def reduce(buf):
+            slots[rank] = buf.copy()
+            bar.wait()
+            buf[:] = slots[0] + slots[1]
+            bar.wait()
+        return reduce
+
+    for r, tr in enumerate(ranks):
+        tr.set_host_reducer(reducer(r), r, 2)
+    mask = T.trainable_mask(blocks, filters)
+    m = np.zeros_like(w)
+    v = np.zeros_like(w)
+    want = w.copy()
+    for step, it in enumerate([3, 12]):
+        gs, ps = [], []
+        for r, tr in enumerate(ranks):
+            tr.compute_gradients(planes[r * n:(r + 1) * n], tpol[r * n:(r + 1) * n], tval[r * n:(r + 1) * n])
+            gs.append(tr.grads())
+            ps.append(tr.params())           # running statistics moved by this rank's forward
+        lr = A.get_cyclical_lr(it)
+        errs = []
+        th = [threading.Thread(target=lambda tr=tr: errs.append(tr.apply(lr))) for tr in ranks]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=120)
+        assert errs == [None, None]
+        assert np.array_equal(ps[0][mask], want[mask]) and np.array_equal(ps[1][mask], want[mask])
+        want, m, v = T.adamw_step(want, gs[0] + gs[1], m, v, mask, step + 1, lr, world=2)
+        stats = ~mask
+        want[stats] = (ps[0][stats] + ps[1][stats]) * np.float32(0.5)
+        got0, got1 = ranks[0].params(), ranks[1].params()
+        assert np.array_equal(got0, got1)
+        assert np.array_equal(got0, want), np.abs(got0 - want).max()
+    assert not np.array_equal(gs[0], gs[1])     # the ranks saw different data
