@@ -299,7 +299,7 @@ __device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
                                           const float* __restrict__ bias,
                                           f32x4 (&wr)[WinoCfg<F>::PF][WinoCfg<F>::XS][WinoCfg<F>::NN], int w,
                                           int lane, f32x4 (&y)[WinoCfg<F>::NN][4], bool pre = false,
-                                          unsigned long long* tr = nullptr) {
+                                          unsigned long long* tr = nullptr, int* vctr = nullptr, int vtarget = 0) {
     constexpr int CF = F / 16;
     constexpr int NWV = WinoCfg<F>::NWV, NN = WinoCfg<F>::NN, XS = WinoCfg<F>::XS;
     constexpr int CH = WinoCfg<F>::CH, VBYTES = CH * 1024, XST = CH * 64;   // V buffer, xi stride
@@ -404,7 +404,14 @@ __device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
             if (st == 4) wino_stamp(tr, 20 + c);
             if constexpr (F == 256) {
                 (void)dn;
-                if (st == SPX - 1 && more && w < NWV / 2) xf.both(c + 1, (c + 1) & 1);
+                if (st == SPX - 1 && more && w < NWV / 2) {
+                    // flow boundary (vctr): chunk 1 goes into V[1], which the previous conv's last
+                    // chunk used -- wait until every wave has counted its reads of it done
+                    if (c == 0 && vctr)
+                        while (__hip_atomic_load(vctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < vtarget)
+                            __builtin_amdgcn_s_sleep(1);
+                    xf.both(c + 1, (c + 1) & 1);
+                }
             } else {
                 constexpr int TSG = (WINO_TSTAG + WINO_TSPLIT) / XS < SPX ? WINO_TSTAG : 0;
                 const bool late = TSG > 0 && w >= NWV / 2;
@@ -419,6 +426,9 @@ __device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
         // ordered by the previous chunk's barrier, so the waves that finish first start their
         // output transform beside the others' last MFMAs (C3 A/B: tower -0.6 %)
         if (more) __syncthreads();
+        // flow boundary: this wave's reads of the last chunk's V buffer are done (release: they have
+        // returned before another wave's transform may overwrite it)
+        else if (vctr && lane == 0) __hip_atomic_fetch_add(vctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         wino_stamp(tr, 2 + c);
     }
     // output transform Y = A^T M A per (output fragment n, channel pair), + bias: the two channels

@@ -534,7 +534,9 @@ def main():
         algo_bytes = wb + (rows / launches) * (80.0 + 218 * 4.0 + 4.0)
         return {"bound": "mfma", "achieved": exec_tflops, "peak": peak, "unit": "TFLOP/s",
                 "frac": exec_tflops / peak, "traffic": traffic,
-                "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
+                "traffic_unit": "bytes/launch past L2 (PMC FETCH_SIZE x2 + WRITE_SIZE: L2-miss fabric requests, "
+                                "Infinity-Cache hits included -- an upper bound on HBM bytes)",
+                "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "traffic_ratio": (traffic / algo_bytes) if traffic else None,
                 "kernel": "%s: input conv + %d residual convs + heads in one launch, %s; %d launches timed (HIP events "
