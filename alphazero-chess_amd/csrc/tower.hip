@@ -985,7 +985,17 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase,
     int* vctr = nullptr;
     const int vtarget = 0;
 #endif
-    wino_core<F>(ldsb, vbase + (F == 64 ? vsel * VBYTES : 0), rW, rN, bias, wr, w, lane, y, pre_in, tr, vctr, vtarget);
+#ifdef AZ_WINO64_ROT
+    // F = 64: quarters in rotated order, each wave's own first; flag[q] = the last conv whose V
+    // quarter q wave q has written (monotone); the first conv transforms behind its own barrier
+    const int rotw = F == 64 ? w : 0;
+    const int* qflag = F == 64 && pre_in ? flag : nullptr;
+#else
+    const int rotw = 0;
+    const int* qflag = nullptr;
+#endif
+    wino_core<F>(ldsb, vbase + (F == 64 ? vsel * VBYTES : 0), rW, rN, bias, wr, w, lane, y, pre_in, tr, vctr, vtarget,
+                 rotw, qflag, seq);
     wino_stamp(tr, 10);
     f32x4 o[NN][4];
 #pragma unroll
@@ -1027,8 +1037,16 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase,
         // F = 64: each wave's 16 output channels are a quarter of the next conv's single chunk;
         // the wave transforms them from its registers (DPP neighbour exchange) into the other V
         // buffer -- no ACT round trip, no barrier between the epilogue and the transform
-        (void)flag; (void)seq;
         if (pre_out) wino_xform_regs<F>(o[0], ldsb + vbase + (1 - vsel) * VBYTES, w, lane);
+#ifdef AZ_WINO64_ROT
+        // publish this wave's quarter of the next conv's V; no barrier: the next conv starts on it
+        if (pre_out) {
+            if (lane == 0) __hip_atomic_store(flag + w, seq + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            return;
+        }
+#else
+        (void)flag; (void)seq;
+#endif
     } else {
         (void)pre_out; (void)flag; (void)seq;
     }
@@ -1100,7 +1118,7 @@ __device__ __forceinline__ void tower32w_board(const float* __restrict__ planes,
 #pragma unroll
                 for (int n = 0; n < NN; n++)
                     wring[i][xs][n] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                                    r, voff + n * 1024 + wino_toff<F>(0, i * XS + xs), 0, 0));
+                                                                    r, voff + n * 1024 + wino_toff<F>(0, wino_rot0<F>(i * XS + xs, w)), 0, 0));
     }
     for (int b = 0; b < ta.blocks; b++) {
         const unsigned wb3 = b + 1 < ta.blocks ? ta.wwbytes[2 * b + 2] : 0u;   // after the last conv: nothing (reads 0)

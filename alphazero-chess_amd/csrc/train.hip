@@ -362,6 +362,67 @@ colsum_kernel(const float* __restrict__ V, int ld, int C, int R, const float* __
     }
 }
 
+// The same sums four channels per thread (16-byte loads; C and ld multiples of 4): thread
+// (phase p = tid / 16, quad q = tid % 16) sums rows rbeg + p, rbeg + p + 16, ... of channels
+// 64 blockIdx.y + 4 q .. + 3, phases combined in order.  16 phases instead of 4 keep 4x more loads in
+// flight (MODE 2, three streams and a division per element: 41 -> ? us per launch at 32768 x 256).
+template <int MODE>
+__global__ void __launch_bounds__(256)
+colsum4_kernel(const float* __restrict__ V, int ld, int C, int R, const float* __restrict__ mean,
+               const float* __restrict__ stdv, const float* __restrict__ O, const float* __restrict__ Y,
+               float* __restrict__ part) {
+    __shared__ float4 sh[2][16][16];
+    const int tid = threadIdx.x, p = tid >> 4, q = tid & 15, c = blockIdx.y * 64 + 4 * q;
+    const int rbeg = blockIdx.x * CS_ROWS, rend = min(R, rbeg + CS_ROWS);
+    float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
+    if (c < C) {
+        const float4 mu = (MODE >= 1) ? *reinterpret_cast<const float4*>(mean + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 sd = (MODE == 2) ? *reinterpret_cast<const float4*>(stdv + c) : make_float4(1.f, 1.f, 1.f, 1.f);
+#pragma unroll 4
+        for (int r = rbeg + p; r < rend; r += 16) {
+            const size_t e = (size_t)r * ld + c;
+            const float4 v = *reinterpret_cast<const float4*>(V + e);
+            if constexpr (MODE == 0) {
+                s0.x += v.x; s0.y += v.y; s0.z += v.z; s0.w += v.w;
+            } else if constexpr (MODE == 1) {
+                const float dx = v.x - mu.x, dy = v.y - mu.y, dz = v.z - mu.z, dw = v.w - mu.w;
+                s0.x += dx * dx; s0.y += dy * dy; s0.z += dz * dz; s0.w += dw * dw;
+            } else {
+                const float4 o = *reinterpret_cast<const float4*>(O + e), y = *reinterpret_cast<const float4*>(Y + e);
+                const float zx = o.x > 0.0f ? v.x : 0.0f, zy = o.y > 0.0f ? v.y : 0.0f;
+                const float zz = o.z > 0.0f ? v.z : 0.0f, zw = o.w > 0.0f ? v.w : 0.0f;
+                s0.x += zx; s0.y += zy; s0.z += zz; s0.w += zw;
+                s1.x += zx * ((y.x - mu.x) / sd.x); s1.y += zy * ((y.y - mu.y) / sd.y);
+                s1.z += zz * ((y.z - mu.z) / sd.z); s1.w += zw * ((y.w - mu.w) / sd.w);
+            }
+        }
+    }
+    sh[0][p][q] = s0;
+    sh[1][p][q] = s1;
+    __syncthreads();
+    if (tid < 64) {                                    // thread = channel blockIdx.y * 64 + tid
+        const int cq = tid >> 2, k = tid & 3, cc = blockIdx.y * 64 + tid;
+        if (cc < C) {
+            const int nw = MODE == 2 ? 2 : 1;
+            for (int wch = 0; wch < nw; wch++) {
+                float a = 0.0f;
+                for (int ph = 0; ph < 16; ph++) a += reinterpret_cast<const float*>(&sh[wch][ph][cq])[k];
+                part[((size_t)blockIdx.x * 2 + wch) * C + cc] = a;
+            }
+        }
+    }
+}
+
+// colsum with 16-byte loads when the channel layout allows it, else the scalar kernel
+template <int MODE>
+void launch_colsum(dim3 g, hipStream_t st, const float* V, int ld, int C, int R, const float* mean, const float* stdv,
+                   const float* O, const float* Y, float* part) {
+    const bool vec = C % 4 == 0 && ld % 4 == 0 && ((uintptr_t)V & 15) == 0 && (!O || ((uintptr_t)O & 15) == 0) &&
+                     (!Y || ((uintptr_t)Y & 15) == 0);
+    if (vec) colsum4_kernel<MODE><<<g, 256, 0, st>>>(V, ld, C, R, mean, stdv, O, Y, part);
+    else colsum_kernel<MODE><<<g, 256, 0, st>>>(V, ld, C, R, mean, stdv, O, Y, part);
+}
+
 // sum the row-block partials of channel c, one wavefront per channel: lane l adds blocks
 // l, l + 64, ... in order, then a fixed butterfly over the lanes -- a fixed order (the step stays
 // bit-reproducible), 64 loads in flight instead of one dependent chain of nblk
@@ -956,9 +1017,9 @@ int bn_forward(Trainer* T, int bi, const float* Y, int ld, int C, int R, size_t 
     float* sd = T->bstd + (size_t)bi * T->slot;
     const int nb = nblk_rows(R);
     dim3 g(nb, (C + 63) / 64);
-    tr::colsum_kernel<0><<<g, 256, 0, T->st>>>(Y, ld, C, R, nullptr, nullptr, nullptr, nullptr, T->cpart);
+    tr::launch_colsum<0>(g, T->st, Y, ld, C, R, nullptr, nullptr, nullptr, nullptr, T->cpart);
     tr::finalize_mean_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(T->cpart, nb, C, R, mean);
-    tr::colsum_kernel<1><<<g, 256, 0, T->st>>>(Y, ld, C, R, mean, nullptr, nullptr, nullptr, T->cpart);
+    tr::launch_colsum<1>(g, T->st, Y, ld, C, R, mean, nullptr, nullptr, nullptr, T->cpart);
     tr::finalize_var_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(T->cpart, nb, C, R, mean, sd, P + 2 * C, P + 3 * C);
     tr::bn_apply_kernel<<<grid_for((size_t)R * C), 256, 0, T->st>>>(Y, ld, C, R, mean, sd, P, P + C, res, out);
     return hipGetLastError() == hipSuccess ? 0 : fail("bn forward failed");
@@ -971,7 +1032,7 @@ int bn_backward(Trainer* T, int bi, const float* dout, const float* O, const flo
     const float* sd = T->bstd + (size_t)bi * T->slot;
     const int nb = nblk_rows(R);
     dim3 g(nb, (C + 63) / 64);
-    tr::colsum_kernel<2><<<g, 256, 0, T->st>>>(dout, ld, C, R, mean, sd, O, Y, T->cpart);
+    tr::launch_colsum<2>(g, T->st, dout, ld, C, R, mean, sd, O, Y, T->cpart);
     float* dgam = T->g + bn_off;
     float* dbet = T->g + bn_off + C;
     tr::finalize_bnback_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(T->cpart, nb, C, dgam, dbet);
@@ -983,7 +1044,7 @@ int bn_backward(Trainer* T, int bi, const float* dout, const float* O, const flo
 int bias_grad(Trainer* T, const float* dy, int ld, int C, int R, float* dst) {
     const int nb = nblk_rows(R);
     dim3 g(nb, (C + 63) / 64);
-    tr::colsum_kernel<0><<<g, 256, 0, T->st>>>(dy, ld, C, R, nullptr, nullptr, nullptr, nullptr, T->cpart);
+    tr::launch_colsum<0>(g, T->st, dy, ld, C, R, nullptr, nullptr, nullptr, nullptr, T->cpart);
     tr::finalize_sum_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(T->cpart, nb, C, dst);
     return hipGetLastError() == hipSuccess ? 0 : fail("bias grad failed");
 }

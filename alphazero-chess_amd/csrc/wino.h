@@ -98,6 +98,15 @@ template <> struct WinoCfg<64> { static constexpr int NWV = 4, NN = 1, XS = 2, C
 template <int F> __device__ __forceinline__ int wino_voff(int w, int lane) {
     return (WinoCfg<F>::NN * w * 64 + lane) * 16;
 }
+// the first conv's ring steps under the F = 64 k-rotation (AZ_WINO64_ROT: wave w starts on its own
+// channel quarter w); the identity otherwise
+template <int F> __device__ __forceinline__ int wino_rot0(int t, int w) {
+#ifdef AZ_WINO64_ROT
+    if constexpr (F == 64) return (((t / 16) + w) & 3) * 16 + t % 16;
+#endif
+    (void)w;
+    return t;
+}
 template <int F> __device__ __forceinline__ int wino_toff(int cg, int t) {
     constexpr int KPC = WinoCfg<F>::CH / 16, CF = F / 16;
     return ((cg * KPC + t / 16) * 16 + t % 16) * CF * 1024;
@@ -299,7 +308,8 @@ __device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
                                           const float* __restrict__ bias,
                                           f32x4 (&wr)[WinoCfg<F>::PF][WinoCfg<F>::XS][WinoCfg<F>::NN], int w,
                                           int lane, f32x4 (&y)[WinoCfg<F>::NN][4], bool pre = false,
-                                          unsigned long long* tr = nullptr, int* vctr = nullptr, int vtarget = 0) {
+                                          unsigned long long* tr = nullptr, int* vctr = nullptr, int vtarget = 0,
+                                          int rotw = 0, const int* qflag = nullptr, int qseq = 0) {
     constexpr int CF = F / 16;
     constexpr int NWV = WinoCfg<F>::NWV, NN = WinoCfg<F>::NN, XS = WinoCfg<F>::XS;
     constexpr int CH = WinoCfg<F>::CH, VBYTES = CH * 1024, XST = CH * 64;   // V buffer, xi stride
@@ -344,8 +354,14 @@ __device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
         __syncthreads();
     }
     wino_stamp(tr, 1);
-    // B fragment of this wave's step t: 16-channel group t / 16 of the chunk, point t % 16
-    auto boff = [](int t) { return (t / 16) * 1024 + (t % 16) * XST; };
+    // B fragment of this wave's step t: 16-channel group t / 16 of the chunk, point t % 16.
+    // F = 64 k-rotation (rotw = w, AZ_WINO64_ROT): the wave runs the input channel quarters in the
+    // order w, w + 1, w + 2, w + 3 -- its own quarter of V (transformed by itself from its outputs)
+    // first -- and before its first read of quarter q != w waits until wave q has published it
+    // (qflag[q] >= qseq; qflag = nullptr: no waits, V complete behind a barrier)
+    auto qmap = [rotw](int q) { return (q + rotw) & (KPC - 1); };
+    auto boff = [&](int t) { return qmap(t / 16) * 1024 + (t % 16) * XST; };
+    auto tmap = [&](int T) { return (T / SPC) * SPC + qmap((T % SPC) / 16) * 16 + T % 16; };
 #pragma unroll 1
     for (int c = 0; c < NCHUNK; c++) {
         f32x2 dn[IT][4][2];
@@ -361,6 +377,11 @@ __device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
             for (int xs = 0; xs < XS; xs++) {
                 const int t = st * XS + xs;
                 B[xs] = bq[t % LA];
+                if (qflag && (t + LA) % 16 == 0 && t + LA < SPC) {
+                    const int q = qmap((t + LA) / 16);
+                    while (__hip_atomic_load(qflag + q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < qseq)
+                        __builtin_amdgcn_s_sleep(1);
+                }
                 if (t + LA < SPC) bq[t % LA] = *reinterpret_cast<const f32x4*>(ldsb + vb + boff(t + LA));
             }
             f32x4 a[XS][NN];
@@ -383,7 +404,7 @@ __device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
                     for (int n = 0; n < NN; n++)
                         wr[st % PF][xs][n] = __builtin_bit_cast(
                             f32x4, __builtin_amdgcn_raw_buffer_load_b128(nxt ? rN : rW, voff + n * 1024,
-                                                                         (to + xs) * CF * 1024, 0));
+                                                                         tmap(to + xs) * CF * 1024, 0));
             }
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
