@@ -230,57 +230,88 @@ wgrad_f32_kernel(const float* __restrict__ X, int ldx, int K, const float* __res
             }
 }
 
-// Winograd weight-grad GEMM at F = 256: one workgroup per (row split, point xi) computes the whole
-// 256 x 256 dU[xi] partial over its (board, tile) rows, so each transformed operand is read from
-// HBM once (64 x 64 tiles read each four times and were bound by that traffic).  8 waves, wave w
-// owns co [32 w, 32 w + 32) x all 256 ci: accumulator block (j, c) row m is ci = 64 j + 4 m + c, so
-// one ds_read_b128 of a row feeds four blocks; 32 MFMAs per 4 LDS b128 + 2 b32 reads per 4 rows.
-// Rows are staged WG_R at a time through LDS, the next stage's prefetched into registers beside
-// the current stage's MFMAs.  partial[split][xi][ci][co]; every element sums its split's rows in
-// row order (fixed order; splits reduced in order by reduce_kernel).
-constexpr int WG_R = 16, WG_S = 256 + 16;   // 16 rows per stage: 142 us vs 146 (32), 151 (64), 146 (8)
+// Winograd weight grad at F = 256, transforms fused into the GEMM's staging: one workgroup per
+// (split of 512 (board, tile) rows, point xi = 4 r + q) computes the whole 256 x 256 dU[xi] partial
+// over its rows.  Each stage is one board: the workgroup gathers the 2 x 2 input squares and the
+// 2 x 2 output-gradient squares point xi combines per (tile, channel) -- V[xi] = (B^T d B)[r][q]
+// and M'[xi] = (A dY A^T)[r][q] with the same additions in the same order as
+// wino_wgrad_transform_kernel -- straight from X and dY (the 16 point workgroups of a split share
+// one XCD's L2: workgroup id = split + splits xi), so the 16 transformed operands never go to HBM.
+// GEMM: 8 waves, wave w owns co [32 w, 32 w + 32) x all 256 ci: accumulator block (j, c) row m is
+// ci = 64 j + 4 m + c, so one ds_read_b128 of a row feeds four blocks.  The next board's squares
+// are loaded into registers beside the current board's MFMAs.  partial[split][xi][ci][co]; every
+// element sums its split's rows in row order (fixed order; splits reduced in order by reduce_kernel).
+constexpr int WG_S = 256 + 16;
+// the four F(2x2,3x3) combinations: (a, b) = (e0, e2) / (e1, e2) / (e1, e2) / (e1, e3) of a patch
+// row or column -> a - b, a + b, b - a, a - b (B^T rows)
+__device__ __forceinline__ f32x4 wino_comb(int k, f32x4 a, f32x4 b) { return k == 1 ? a + b : k == 2 ? b - a : a - b; }
 __global__ void __launch_bounds__(512)
-wino_wgrad_gemm_kernel(const float* __restrict__ Vt, const float* __restrict__ Mt, int K, int rows_per_split,
+wino_wgrad_gemm_kernel(const float* __restrict__ X, const float* __restrict__ DY, int K, int rows_per_split,
                        float* __restrict__ partial) {
-    constexpr int F = 256, NV = WG_R * (F / 4) / 512;
-    __shared__ __attribute__((aligned(16))) float xs[WG_R * WG_S];
-    __shared__ __attribute__((aligned(16))) float ds[WG_R * WG_S];
+    constexpr int F = 256;
+    __shared__ __attribute__((aligned(16))) float xs[16 * WG_S];
+    __shared__ __attribute__((aligned(16))) float ds[16 * WG_S];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int split = blockIdx.x, xi = blockIdx.y;
-    const float* X = Vt + (size_t)xi * K * F;
-    const float* D = Mt + (size_t)xi * K * F;
+    const int split = blockIdx.x, xi = blockIdx.y, r = xi >> 2, q = xi & 3;
+    const int i1 = r == 0 ? 0 : 1, i2 = r == 3 ? 3 : 2, j1 = q == 0 ? 0 : 1, j2 = q == 3 ? 3 : 2;
     const int rbeg = split * rows_per_split, rend = min(K, rbeg + rows_per_split);
     f32x4 acc[16][2];
 #pragma unroll
     for (int b = 0; b < 16; b++)
 #pragma unroll
         for (int n = 0; n < 2; n++) acc[b][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float4 xv[NV], dv[NV];
+    // staging: thread = (channel quad c4, tiles 2 tp and 2 tp + 1)
+    const int c4 = (tid & 63) * 4, tp = tid >> 6;
+    f32x4 xd[2][2][2], yv[2][2][2];   // [tile][patch row i1 / i2][patch column j1 / j2], [tile][a][b]
     auto fetch = [&](int rc) {
+        const size_t b64 = (size_t)(rc >> 4) * 64;
 #pragma unroll
-        for (int j = 0; j < NV; j++) {
-            const int i = tid + j * 512, rr = i >> 6, c4 = (i & 63) * 4;
-            xv[j] = dv[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (rc + rr < rend) {
-                xv[j] = *reinterpret_cast<const float4*>(X + (size_t)(rc + rr) * F + c4);
-                dv[j] = *reinterpret_cast<const float4*>(D + (size_t)(rc + rr) * F + c4);
-            }
+        for (int u = 0; u < 2; u++) {
+            const int t = 2 * tp + u, ty = t >> 2, tx = t & 3;
+#pragma unroll
+            for (int ii = 0; ii < 2; ii++)
+#pragma unroll
+                for (int jj = 0; jj < 2; jj++) {
+                    const int row = 2 * ty - 1 + (ii ? i2 : i1), col = 2 * tx - 1 + (jj ? j2 : j1);
+                    xd[u][ii][jj] = ((unsigned)row < 8u && (unsigned)col < 8u)
+                                        ? *reinterpret_cast<const f32x4*>(X + (b64 + row * 8 + col) * F + c4)
+                                        : f32x4{0.f, 0.f, 0.f, 0.f};
+                }
+#pragma unroll
+            for (int a = 0; a < 2; a++)
+#pragma unroll
+                for (int bb = 0; bb < 2; bb++)
+                    yv[u][a][bb] = *reinterpret_cast<const f32x4*>(DY + (b64 + (2 * ty + a) * 8 + 2 * tx + bb) * F + c4);
         }
     };
     if (rbeg < rend) fetch(rbeg);
-    for (int rc = rbeg; rc < rend; rc += WG_R) {
+    for (int rc = rbeg; rc < rend; rc += 16) {
         __syncthreads();
 #pragma unroll
-        for (int j = 0; j < NV; j++) {
-            const int i = tid + j * 512, rr = i >> 6, c4 = (i & 63) * 4;
-            *reinterpret_cast<float4*>(xs + rr * WG_S + c4) = xv[j];
-            *reinterpret_cast<float4*>(ds + rr * WG_S + c4) = dv[j];
+        for (int u = 0; u < 2; u++) {
+            const int t = 2 * tp + u;
+            // V: rows first (tt over the two columns), then the column combination
+            const f32x4 tt1 = wino_comb(r, xd[u][0][0], xd[u][1][0]), tt2 = wino_comb(r, xd[u][0][1], xd[u][1][1]);
+            const f32x4 v = wino_comb(q, tt1, tt2);
+            // M': p_b = (A dY)[r][b], then (p A^T)[q], as ca y0 + cb y1 with the rows of A
+            // {(1, 0), (1, 1), (1, -1), (0, -1)}: every product is by 1, -1 or 0, so the values are
+            // the transform kernel's (signed zeros aside).  The same as a select chain
+            // (r == 0 ? y0 : ... : -y1) was miscompiled for gfx950: r = 3 produced y0 on the GPU
+            // (tools/wgrad_dbg.hip, profiles/r04_wgrad_dbg.log), while a CPU emulation was right.
+            const float ra = r == 3 ? 0.0f : 1.0f, rb = r == 0 ? 0.0f : (r == 1 ? 1.0f : -1.0f);
+            const float qa = q == 3 ? 0.0f : 1.0f, qb = q == 0 ? 0.0f : (q == 1 ? 1.0f : -1.0f);
+            f32x4 p[2];
+#pragma unroll
+            for (int bb = 0; bb < 2; bb++) p[bb] = yv[u][0][bb] * ra + yv[u][1][bb] * rb;
+            const f32x4 m = p[0] * qa + p[1] * qb;
+            *reinterpret_cast<f32x4*>(xs + t * WG_S + c4) = v;
+            *reinterpret_cast<f32x4*>(ds + t * WG_S + c4) = m;
         }
         __syncthreads();
-        if (rc + WG_R < rend) fetch(rc + WG_R);
+        if (rc + 16 < rend) fetch(rc + 16);
 #pragma unroll
-        for (int q = 0; q < WG_R / 4; q++) {
-            const int rq = q * 4 + (lane >> 4);
+        for (int qq = 0; qq < 4; qq++) {
+            const int rq = qq * 4 + (lane >> 4);
             const float b0 = ds[rq * WG_S + 32 * w + (lane & 15)];
             const float b1 = ds[rq * WG_S + 32 * w + 16 + (lane & 15)];
 #pragma unroll
@@ -665,9 +696,13 @@ conv_wino_train_kernel(const float* __restrict__ X, const uint4* __restrict__ U,
 // winograd_f32) of one F x F 3x3 conv in the burn layout w[co][ci][3][3], into the layout
 // wino_core streams ([ci/16][xi][co/16][lane][4]); flip = 1: the data-grad conv's kernel
 // g'[o = ci][i = co][ky][kx] = w[co][ci][2 - ky][2 - kx].  One thread per (output, input) pair.
-__global__ void __launch_bounds__(256) wino_weights_kernel(const float* __restrict__ w, int F, int flip,
-                                                           float* __restrict__ U) {
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+// All residual convs of the step in one launch (80 launches of ~7 us were 2 % of the step):
+// blockIdx.y = 2 conv + flip; conv j's weights at w + j wstride, its U at U + (2 j + flip) ustride.
+__global__ void __launch_bounds__(256) wino_weights_kernel(const float* __restrict__ w0, size_t wstride, int F,
+                                                           float* __restrict__ U0, size_t ustride) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x, flip = blockIdx.y & 1;
+    const float* __restrict__ w = w0 + (blockIdx.y >> 1) * wstride;
+    float* __restrict__ U = U0 + (size_t)blockIdx.y * ustride;
     if (idx >= F * F) return;
     const int o = idx / F, i = idx % F;      // output / input channel of the conv U describes
     double g[3][3];
@@ -707,6 +742,8 @@ __global__ void repack3x3_kernel(const float* __restrict__ w, int co_n, int ci_n
 //   dW[co][ci]     = G^T dU[co][ci] G                                   (U = G g G^T)
 // 2.25x fewer MFMAs than the 9-tap implicit GEMM.  Vt[xi][k][ci], Mt[xi][k][co] with
 // k = board * 16 + tile; one thread per (k, channel), channels fastest (coalesced).
+// Round 4: the training step no longer launches this kernel -- wino_wgrad_gemm_kernel computes the
+// same transforms in its staging -- it stays as the reference of tools/wgrad_dbg.hip.
 __global__ void __launch_bounds__(256) wino_wgrad_transform_kernel(const float* __restrict__ X,
                                                                    const float* __restrict__ DY, int F, int B,
                                                                    float* __restrict__ Vt, float* __restrict__ Mt) {
@@ -882,9 +919,10 @@ struct Trainer {
     std::vector<float*> wf, wd;
     // Winograd weights of the residual convs (F = 256): forward and data grad (env AZ_TRAIN_WINOGRAD=0: off)
     bool wino = false;
-    std::vector<float*> uf, ud;
+    std::vector<float*> uf, ud;              // conv i's forward / data-grad U: ubase + (2 (i - 1) + {0, 1}) ubytes
+    float* ubase = nullptr;
     size_t ubytes = 0;
-    float *wvt = nullptr, *wmt = nullptr, *wdu = nullptr;   // Winograd weight-grad transforms, dU
+    float* wdu = nullptr;                    // Winograd weight grad dU [16][F][F]
     float *w40f = nullptr, *w40d = nullptr, *b40 = nullptr, *wp2f = nullptr, *w1d = nullptr;
     // saved activations (R = B*64 rows)
     float* x0 = nullptr;                     // [R][64] input planes
@@ -932,7 +970,6 @@ struct Trainer {
 namespace {
 
 constexpr int ROWS_PER_SPLIT = 512;   // weight-grad row split (8 boards)
-constexpr int WINO_ROWS_PER_SPLIT = 2048;   // Winograd weight grad: (board, tile) rows per split
 
 int launch_conv(Trainer* T, int taps, const float* X, int ldx, int K, const float* W, int N, const float* bias,
                 const float* addend, float* Y, int ldy, int R) {
@@ -978,29 +1015,19 @@ int launch_wgrad(Trainer* T, int taps, const float* X, int ldx, int K, const flo
 }
 
 // Winograd weight grad of a residual F x F conv (input X, output gradient DY, B boards) into g
-int wino_rows_per_split(int B) { return B * 16 >= 8192 ? WINO_ROWS_PER_SPLIT : ROWS_PER_SPLIT; }
-size_t wino_splits(int B) { return (size_t)((B * 16 + wino_rows_per_split(B) - 1) / wino_rows_per_split(B)); }
 // F = 256 (wino_wgrad_gemm_kernel): 512 rows per split, 16 x 16 = 256 workgroups at B = 512
 constexpr int WINO_GEMM_ROWS = 512;
 size_t wino_gemm_splits(int B) { return (size_t)((B * 16 + WINO_GEMM_ROWS - 1) / WINO_GEMM_ROWS); }
+// Winograd weight grad (F = 256, the only Winograd training width: T->wino): the transforms fused
+// into the GEMM's staging (wino_wgrad_gemm_kernel), the splits summed in order, dW = G^T dU G
 int launch_wino_wgrad(Trainer* T, const float* X, const float* DY, int B, float* g) {
     const int F = T->F, K = B * 16;
+    if (F != 256) return fail("Winograd wgrad: F = 256 only");
     if (B > T->Bmax) return fail("Winograd wgrad: batch too large");
-    if (wino_splits(B) * 16 * (size_t)F * F > T->wpart_cap) return fail("Winograd wgrad: partial buffer too small");
+    const int splits = (int)wino_gemm_splits(B);
+    if (splits * 16 * (size_t)F * F > T->wpart_cap) return fail("Winograd wgrad: partial buffer too small");
     hipStream_t st = T->st;
-    tr::wino_wgrad_transform_kernel<<<grid_for((size_t)K * F), 256, 0, st>>>(X, DY, F, B, T->wvt, T->wmt);
-    int splits;
-    if (F == 256) {
-        splits = (int)wino_gemm_splits(B);
-        if (splits * 16 * (size_t)F * F > T->wpart_cap) return fail("Winograd wgrad: partial buffer too small");
-        tr::wino_wgrad_gemm_kernel<<<dim3(splits, 16), 512, 0, st>>>(T->wvt, T->wmt, K, WINO_GEMM_ROWS, T->wpart);
-    } else {
-        const int rps = wino_rows_per_split(B);
-        splits = (int)wino_splits(B);
-        dim3 grid(F / tr::GK, F / tr::GN, splits * 16);
-        tr::wgrad_f32_kernel<1><<<grid, 256, 0, st>>>(T->wvt, F, F, T->wmt, F, F, K, rps, T->wpart, 16, (size_t)K * F,
-                                                      (size_t)K * F);
-    }
+    tr::wino_wgrad_gemm_kernel<<<dim3(splits, 16), 512, 0, st>>>(X, DY, K, WINO_GEMM_ROWS, T->wpart);
     const size_t n = (size_t)16 * F * F;
     tr::reduce_kernel<<<grid_for(n), 256, 0, st>>>(T->wpart, splits, n, T->wdu);
     tr::wino_wgrad_out_kernel<<<grid_for((size_t)F * F), 256, 0, st>>>(T->wdu, F, g);
@@ -1064,13 +1091,14 @@ int trainer_grads(Trainer* T, const float* planes, const float* tpol, const floa
     AZ_HIP(hipMemcpyAsync(T->tval, tval, (size_t)B * sizeof(float), hipMemcpyHostToDevice, st));
     AZ_HIP(hipMemsetAsync(T->g, 0, T->np * sizeof(float), st));
     // weights of this step in GEMM layouts
+    if (T->wino && T->blocks > 0) {  // residual convs: Winograd weights, forward and data grad, one launch
+        const size_t wstride = L.tower.size() > 2 ? L.tower[2].w - L.tower[1].w : 0;
+        tr::wino_weights_kernel<<<dim3((unsigned)((F * F + 255) / 256), 2 * (L.tower.size() - 1)), 256, 0, st>>>(
+            T->p + L.tower[1].w, wstride, F, T->ubase, T->ubytes / sizeof(float));
+    }
     for (size_t i = 0; i < L.tower.size(); i++) {
         const auto& c = L.tower[i];
-        if (i > 0 && T->wino) {      // residual convs: Winograd weights, forward and data grad
-            tr::wino_weights_kernel<<<grid_for((size_t)F * F), 256, 0, st>>>(T->p + c.w, F, 0, T->uf[i]);
-            tr::wino_weights_kernel<<<grid_for((size_t)F * F), 256, 0, st>>>(T->p + c.w, F, 1, T->ud[i]);
-            continue;
-        }
+        if (i > 0 && T->wino) continue;
         const int kpad = i == 0 ? 64 : F;
         tr::repack3x3_kernel<<<grid_for((size_t)9 * kpad * F), 256, 0, st>>>(T->p + c.w, F, c.cin, kpad, T->wf[i],
                                                                            i == 0 ? nullptr : T->wd[i]);
@@ -1292,12 +1320,13 @@ int az_trainer_create(int blocks, int filters, const float* weights, size_t n, i
     // Winograd U per residual conv: 16 points x F x F + 8 zero ring steps of prefetch pad
     const size_t ufl = (size_t)16 * F * F + (size_t)8 * (F / 16) * 64 * 4;
     T->ubytes = ufl * sizeof(float);
+    if (T->wino && nconv > 1) T->ubase = A(2 * (size_t)(nconv - 1) * ufl);
     for (int i = 0; i < nconv; i++) {
         const bool w9 = i == 0 || !T->wino;
         T->wf.push_back(w9 ? A((size_t)9 * (i == 0 ? 64 : F) * F) : nullptr);
         T->wd.push_back(i == 0 || !w9 ? nullptr : A((size_t)9 * F * F));
-        T->uf.push_back(i > 0 && T->wino ? A(ufl) : nullptr);
-        T->ud.push_back(i > 0 && T->wino ? A(ufl) : nullptr);
+        T->uf.push_back(i > 0 && T->ubase ? T->ubase + (size_t)(2 * (i - 1)) * ufl : nullptr);
+        T->ud.push_back(i > 0 && T->ubase ? T->ubase + (size_t)(2 * (i - 1) + 1) * ufl : nullptr);
     }
     T->w40f = A((size_t)F * 64); T->w40d = A((size_t)64 * F); T->b40 = A(64); T->wp2f = A(32 * 64); T->w1d = A(64 * 512);
     T->x0 = A(R * 64);
@@ -1319,9 +1348,7 @@ int az_trainer_create(int blocks, int filters, const float* weights, size_t n, i
     wp = std::max(wp, s1 * 32 * 64);                                    // policy_conv_2
     wp = std::max(wp, sl * 512 * 64);                                   // value_linear_1
     if (T->wino) {   // Winograd weight grads: [16][Bmax * 16][F] transforms, dU [16][F][F]
-        wp = std::max(wp, std::max(wino_splits(max_batch), wino_gemm_splits(max_batch)) * 16 * (size_t)F * F);
-        T->wvt = A((size_t)16 * max_batch * 16 * F);
-        T->wmt = A((size_t)16 * max_batch * 16 * F);
+        wp = std::max(wp, wino_gemm_splits(max_batch) * 16 * (size_t)F * F);
         T->wdu = A((size_t)16 * F * F);
     }
     T->wpart = A(wp);
@@ -1358,12 +1385,9 @@ int az_trainer_create(int blocks, int filters, const float* weights, size_t n, i
         return fail("az_trainer_create: upload failed");
     }
     // the Winograd weight buffers' prefetch pad stays zero (the per-step transforms write the rest)
-    for (size_t i = 0; i < T->uf.size(); i++) {
-        if (!T->uf[i]) continue;
-        if (hipMemset(T->uf[i], 0, T->ubytes) != hipSuccess || hipMemset(T->ud[i], 0, T->ubytes) != hipSuccess) {
-            delete T;
-            return fail("az_trainer_create: upload failed");
-        }
+    if (T->ubase && hipMemset(T->ubase, 0, 2 * (size_t)(nconv - 1) * T->ubytes) != hipSuccess) {
+        delete T;
+        return fail("az_trainer_create: upload failed");
     }
     *out = new az_trainer{T};
     return 0;

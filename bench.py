@@ -86,13 +86,13 @@ def cpu_baseline(blocks, filters, threads, games, sims):
                      % (games, sims, blocks, filters, threads, dt),
            "evals": nevals}
     rnet = O.RefNet(blocks, filters, w)
-    pcfg = O.make_cfg(sims=max(sims // 2, 1), noise=True, seed=42, eval_kind=1, net=rnet, threads=threads)
+    pcfg = O.make_cfg(sims=max(sims // 4, 1), noise=True, seed=42, eval_kind=1, net=rnet, threads=threads)
     t0 = time.perf_counter()
     _, psims, _ = O.selfplay(pcfg, 16, max_plies=1)
     pdt = time.perf_counter() - t0
     out["per_game_port"] = {"value": psims / pdt, "unit": "sims/s", "cores": threads,
                             "sample": "16 games x 1 move x %d sims, one leaf per game at a time, naive C "
-                                      "convolution (oracle/net_ref.c), %.1f s" % (max(sims // 2, 1), pdt)}
+                                      "convolution (oracle/net_ref.c), %.1f s" % (max(sims // 4, 1), pdt)}
     return out
 
 

@@ -64,12 +64,20 @@ fused_kernel(const float* __restrict__ X, const float* __restrict__ DY, int K, i
             const f32x4 tt1 = wino_comb(r, xd[u][0][0], xd[u][1][0]), tt2 = wino_comb(r, xd[u][0][1], xd[u][1][1]);
             const f32x4 v = wino_comb(q, tt1, tt2);
             f32x4 p[2];
+            if constexpr (VARIANT == 0) {   // the select chain the patch used (miscompiled: r = 3 gives y0)
 #pragma unroll
-            for (int bb = 0; bb < 2; bb++) {
-                const f32x4 y0 = yv[u][0][bb], y1 = yv[u][1][bb];
-                p[bb] = r == 0 ? y0 : r == 1 ? y0 + y1 : r == 2 ? y0 - y1 : -y1;
+                for (int bb = 0; bb < 2; bb++) {
+                    const f32x4 y0 = yv[u][0][bb], y1 = yv[u][1][bb];
+                    p[bb] = r == 0 ? y0 : r == 1 ? y0 + y1 : r == 2 ? y0 - y1 : -y1;
+                }
+            } else {                        // coefficient form (train.hip)
+                const float ra = r == 3 ? 0.0f : 1.0f, rb = r == 0 ? 0.0f : (r == 1 ? 1.0f : -1.0f);
+#pragma unroll
+                for (int bb = 0; bb < 2; bb++) p[bb] = yv[u][0][bb] * ra + yv[u][1][bb] * rb;
             }
-            const f32x4 m = q == 0 ? p[0] : q == 1 ? p[0] + p[1] : q == 2 ? p[0] - p[1] : -p[1];
+            const float qa = q == 3 ? 0.0f : 1.0f, qb = q == 0 ? 0.0f : (q == 1 ? 1.0f : -1.0f);
+            const f32x4 m = VARIANT == 0 ? (q == 0 ? p[0] : q == 1 ? p[0] + p[1] : q == 2 ? p[0] - p[1] : -p[1])
+                                         : p[0] * qa + p[1] * qb;
             *reinterpret_cast<f32x4*>(xs + t * WG_S + c4) = v;
             *reinterpret_cast<f32x4*>(ds + t * WG_S + c4) = m;
         }
@@ -127,7 +135,10 @@ int main() {
     hipMemcpy(d, hd.data(), hd.size() * 4, hipMemcpyHostToDevice);
     azi::tr::wino_wgrad_transform_kernel<<<64, 256>>>(x, d, F, B, vt, mt);
     azi::tr::wino_wgrad_gemm_kernel<<<dim3(1, 16), 512>>>(vt, mt, K, 512, part2);    // the committed GEMM
-    dbg::fused_kernel<0><<<dim3(1, 16), 512>>>(x, d, K, 512, part, dump);
+    const int variant = getenv("WGDBG_VARIANT") ? atoi(getenv("WGDBG_VARIANT")) : 0;
+    if (variant) dbg::fused_kernel<1><<<dim3(1, 16), 512>>>(x, d, K, 512, part, dump);
+    else dbg::fused_kernel<0><<<dim3(1, 16), 512>>>(x, d, K, 512, part, dump);
+    printf("variant %d (%s)\n", variant, variant ? "coefficients" : "select chain");
     if (hipDeviceSynchronize() != hipSuccess) { printf("kernel failed\n"); return 2; }
     std::vector<float> hv((size_t)16 * K * F), hm((size_t)16 * K * F), hp((size_t)16 * F * F), hp2(hp.size()),
         hdump((size_t)16 * 2 * 16 * 256);
