@@ -973,29 +973,7 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase,
     f32x4 y[NN][4];
     wino_stamp(tr, 0);
     // F = 64: the single chunk's V alternates between two buffers from conv to conv (vsel)
-#ifdef AZ_WINO_FLOWB
-    // flow boundary (F = 256): flag[1] counts the waves done reading a conv's last V buffer, flag[2]
-    // the leading waves done transforming the next conv's chunk 0 (both monotone over the tower)
-    int* vctr = F == 256 ? flag + 1 : nullptr;
-    const int vtarget = F == 256 ? WinoCfg<F>::NWV * (seq - 1) : 0;
-    if (F == 256 && pre_in)                              // this conv's chunk 0 in V[0], transformed by waves 0-3
-        while (__hip_atomic_load(flag + 2, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 4 * (seq - 1))
-            __builtin_amdgcn_s_sleep(1);
-#else
-    int* vctr = nullptr;
-    const int vtarget = 0;
-#endif
-#ifdef AZ_WINO64_ROT
-    // F = 64: quarters in rotated order, each wave's own first; flag[q] = the last conv whose V
-    // quarter q wave q has written (monotone); the first conv transforms behind its own barrier
-    const int rotw = F == 64 ? w : 0;
-    const int* qflag = F == 64 && pre_in ? flag : nullptr;
-#else
-    const int rotw = 0;
-    const int* qflag = nullptr;
-#endif
-    wino_core<F>(ldsb, vbase + (F == 64 ? vsel * VBYTES : 0), rW, rN, bias, wr, w, lane, y, pre_in, tr, vctr, vtarget,
-                 rotw, qflag, seq);
+    wino_core<F>(ldsb, vbase + (F == 64 ? vsel * VBYTES : 0), rW, rN, bias, wr, w, lane, y, pre_in, tr);
     wino_stamp(tr, 10);
     f32x4 o[NN][4];
 #pragma unroll
@@ -1022,31 +1000,13 @@ __device__ __forceinline__ void conv_wino(char* __restrict__ ldsb, int vbase,
                 while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != seq)
                     __builtin_amdgcn_s_sleep(1);
             WinoXf<F>(ldsb, vbase, w, lane).both(0, 0);
-#ifdef AZ_WINO_FLOWB
-            if (lane == 0) __hip_atomic_fetch_add(flag + 2, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
         }
-#ifdef AZ_WINO_FLOWB
-        // flow boundary: no workgroup barrier -- the next conv's chunk 0 starts once its V is ready
-        // (flag[2]), its chunk 1 transform once the last V buffer is free (flag[1]); the chunk 0
-        // barrier inside the next wino_core re-joins the waves.  The last conv (no pre_out) keeps
-        // the barrier before the heads.
-        if (pre_out) return;
-#endif
     } else if constexpr (F == 64) {
         // F = 64: each wave's 16 output channels are a quarter of the next conv's single chunk;
         // the wave transforms them from its registers (DPP neighbour exchange) into the other V
         // buffer -- no ACT round trip, no barrier between the epilogue and the transform
         if (pre_out) wino_xform_regs<F>(o[0], ldsb + vbase + (1 - vsel) * VBYTES, w, lane);
-#ifdef AZ_WINO64_ROT
-        // publish this wave's quarter of the next conv's V; no barrier: the next conv starts on it
-        if (pre_out) {
-            if (lane == 0) __hip_atomic_store(flag + w, seq + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            return;
-        }
-#else
         (void)flag; (void)seq;
-#endif
     } else {
         (void)pre_out; (void)flag; (void)seq;
     }
@@ -1118,7 +1078,7 @@ __device__ __forceinline__ void tower32w_board(const float* __restrict__ planes,
 #pragma unroll
                 for (int n = 0; n < NN; n++)
                     wring[i][xs][n] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                                    r, voff + n * 1024 + wino_toff<F>(0, wino_rot0<F>(i * XS + xs, w)), 0, 0));
+                                                                    r, voff + n * 1024 + wino_toff<F>(0, i * XS + xs), 0, 0));
     }
     for (int b = 0; b < ta.blocks; b++) {
         const unsigned wb3 = b + 1 < ta.blocks ? ta.wwbytes[2 * b + 2] : 0u;   // after the last conv: nothing (reads 0)

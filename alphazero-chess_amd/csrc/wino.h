@@ -98,15 +98,6 @@ template <> struct WinoCfg<64> { static constexpr int NWV = 4, NN = 1, XS = 2, C
 template <int F> __device__ __forceinline__ int wino_voff(int w, int lane) {
     return (WinoCfg<F>::NN * w * 64 + lane) * 16;
 }
-// the first conv's ring steps under the F = 64 k-rotation (AZ_WINO64_ROT: wave w starts on its own
-// channel quarter w); the identity otherwise
-template <int F> __device__ __forceinline__ int wino_rot0(int t, int w) {
-#ifdef AZ_WINO64_ROT
-    if constexpr (F == 64) return (((t / 16) + w) & 3) * 16 + t % 16;
-#endif
-    (void)w;
-    return t;
-}
 template <int F> __device__ __forceinline__ int wino_toff(int cg, int t) {
     constexpr int KPC = WinoCfg<F>::CH / 16, CF = F / 16;
     return ((cg * KPC + t / 16) * 16 + t % 16) * CF * 1024;
@@ -308,8 +299,7 @@ __device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
                                           const float* __restrict__ bias,
                                           f32x4 (&wr)[WinoCfg<F>::PF][WinoCfg<F>::XS][WinoCfg<F>::NN], int w,
                                           int lane, f32x4 (&y)[WinoCfg<F>::NN][4], bool pre = false,
-                                          unsigned long long* tr = nullptr, int* vctr = nullptr, int vtarget = 0,
-                                          int rotw = 0, const int* qflag = nullptr, int qseq = 0) {
+                                          unsigned long long* tr = nullptr) {
     constexpr int CF = F / 16;
     constexpr int NWV = WinoCfg<F>::NWV, NN = WinoCfg<F>::NN, XS = WinoCfg<F>::XS;
     constexpr int CH = WinoCfg<F>::CH, VBYTES = CH * 1024, XST = CH * 64;   // V buffer, xi stride
@@ -354,14 +344,8 @@ __device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
         __syncthreads();
     }
     wino_stamp(tr, 1);
-    // B fragment of this wave's step t: 16-channel group t / 16 of the chunk, point t % 16.
-    // F = 64 k-rotation (rotw = w, AZ_WINO64_ROT): the wave runs the input channel quarters in the
-    // order w, w + 1, w + 2, w + 3 -- its own quarter of V (transformed by itself from its outputs)
-    // first -- and before its first read of quarter q != w waits until wave q has published it
-    // (qflag[q] >= qseq; qflag = nullptr: no waits, V complete behind a barrier)
-    auto qmap = [rotw](int q) { return (q + rotw) & (KPC - 1); };
-    auto boff = [&](int t) { return qmap(t / 16) * 1024 + (t % 16) * XST; };
-    auto tmap = [&](int T) { return (T / SPC) * SPC + qmap((T % SPC) / 16) * 16 + T % 16; };
+    // B fragment of this wave's step t: 16-channel group t / 16 of the chunk, point t % 16
+    auto boff = [](int t) { return (t / 16) * 1024 + (t % 16) * XST; };
 #pragma unroll 1
     for (int c = 0; c < NCHUNK; c++) {
         f32x2 dn[IT][4][2];
@@ -377,11 +361,6 @@ __device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
             for (int xs = 0; xs < XS; xs++) {
                 const int t = st * XS + xs;
                 B[xs] = bq[t % LA];
-                if (qflag && (t + LA) % 16 == 0 && t + LA < SPC) {
-                    const int q = qmap((t + LA) / 16);
-                    while (__hip_atomic_load(qflag + q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < qseq)
-                        __builtin_amdgcn_s_sleep(1);
-                }
                 if (t + LA < SPC) bq[t % LA] = *reinterpret_cast<const f32x4*>(ldsb + vb + boff(t + LA));
             }
             f32x4 a[XS][NN];
@@ -404,7 +383,7 @@ __device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
                     for (int n = 0; n < NN; n++)
                         wr[st % PF][xs][n] = __builtin_bit_cast(
                             f32x4, __builtin_amdgcn_raw_buffer_load_b128(nxt ? rN : rW, voff + n * 1024,
-                                                                         tmap(to + xs) * CF * 1024, 0));
+                                                                         (to + xs) * CF * 1024, 0));
             }
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -425,14 +404,7 @@ __device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
             if (st == 4) wino_stamp(tr, 20 + c);
             if constexpr (F == 256) {
                 (void)dn;
-                if (st == SPX - 1 && more && w < NWV / 2) {
-                    // flow boundary (vctr): chunk 1 goes into V[1], which the previous conv's last
-                    // chunk used -- wait until every wave has counted its reads of it done
-                    if (c == 0 && vctr)
-                        while (__hip_atomic_load(vctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < vtarget)
-                            __builtin_amdgcn_s_sleep(1);
-                    xf.both(c + 1, (c + 1) & 1);
-                }
+                if (st == SPX - 1 && more && w < NWV / 2) xf.both(c + 1, (c + 1) & 1);
             } else {
                 constexpr int TSG = (WINO_TSTAG + WINO_TSPLIT) / XS < SPX ? WINO_TSTAG : 0;
                 const bool late = TSG > 0 && w >= NWV / 2;
@@ -447,9 +419,6 @@ __device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
         // ordered by the previous chunk's barrier, so the waves that finish first start their
         // output transform beside the others' last MFMAs (C3 A/B: tower -0.6 %)
         if (more) __syncthreads();
-        // flow boundary: this wave's reads of the last chunk's V buffer are done (release: they have
-        // returned before another wave's transform may overwrite it)
-        else if (vctr && lane == 0) __hip_atomic_fetch_add(vctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         wino_stamp(tr, 2 + c);
     }
     // output transform Y = A^T M A per (output fragment n, channel pair), + bias: the two channels
