@@ -23,6 +23,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <initializer_list>
 #include <string>
 #include <vector>
 
@@ -234,8 +235,8 @@ wgrad_f32_kernel(const float* __restrict__ X, int ldx, int K, const float* __res
 // (split of 512 (board, tile) rows, point xi = 4 r + q) computes the whole 256 x 256 dU[xi] partial
 // over its rows.  Each stage is one board: the workgroup gathers the 2 x 2 input squares and the
 // 2 x 2 output-gradient squares point xi combines per (tile, channel) -- V[xi] = (B^T d B)[r][q]
-// and M'[xi] = (A dY A^T)[r][q] with the same additions in the same order as
-// wino_wgrad_transform_kernel -- straight from X and dY (the 16 point workgroups of a split share
+// and M'[xi] = (A dY A^T)[r][q] with the same additions in the same order as the
+// round-3 transform pass (now tools/wgrad_dbg.hip) -- straight from X and dY (the 16 point workgroups of a split share
 // one XCD's L2: workgroup id = split + splits xi), so the 16 transformed operands never go to HBM.
 // GEMM: 8 waves, wave w owns co [32 w, 32 w + 32) x all 256 ci: accumulator block (j, c) row m is
 // ci = 64 j + 4 m + c, so one ds_read_b128 of a row feeds four blocks.  The next board's squares
@@ -354,7 +355,7 @@ __global__ void reduce_kernel(const float* __restrict__ partial, int splits, siz
 //   MODE 0: sum v                       (bias grads, BN mean)
 //   MODE 1: sum (v - mean)^2            (BN biased variance, two-pass like burn)
 //   MODE 2: sum dz, sum dz*yhat with dz = dout*(o > 0), yhat = (y - mean)/std   (BN backward)
-constexpr int CS_ROWS = 256;   // rows per block
+constexpr int CS_ROWS = 128;   // rows per block (256: 8 waves per CU at 32768 rows, colsum4<2> 24 us)
 
 template <int MODE>
 __global__ void __launch_bounds__(256)
@@ -393,6 +394,33 @@ colsum_kernel(const float* __restrict__ V, int ld, int C, int R, const float* __
     }
 }
 
+// What becomes of a column sum once all row blocks are in (the finalize kernels below, or the
+// colsum4 kernel's last block):  SUM a = s0;  MEAN a = s0 / R;  VAR var = s0 / R, a = sqrt(var +
+// eps), b = running mean, c = running var (momentum 0.1, batch mean `mean`);  BNBACK a = dgamma =
+// s1, b = dbeta = s0.  ctr: one arrival counter per 64-channel block, zero between launches.
+enum { FIN_SUM, FIN_MEAN, FIN_VAR, FIN_BNBACK };
+struct ColFin {
+    int kind;
+    float *a, *b, *c;
+    const float* mean;
+    int* ctr;
+};
+__device__ __forceinline__ void fin_store(const ColFin& f, int c, int R, float s0, float s1) {
+    if (f.kind == FIN_SUM) {
+        f.a[c] = s0;
+    } else if (f.kind == FIN_MEAN) {
+        f.a[c] = s0 / (float)R;
+    } else if (f.kind == FIN_VAR) {
+        const float var = s0 / (float)R;
+        f.a[c] = sqrtf(var + 1e-5f);
+        f.b[c] = f.b[c] * 0.9f + f.mean[c] * 0.1f;
+        f.c[c] = f.c[c] * 0.9f + var * 0.1f;
+    } else {
+        f.a[c] = s1;
+        f.b[c] = s0;
+    }
+}
+
 // The same sums four channels per thread (16-byte loads; C and ld multiples of 4): thread
 // (phase p = tid / 16, quad q = tid % 16) sums rows rbeg + p, rbeg + p + 16, ... of channels
 // 64 blockIdx.y + 4 q .. + 3, phases combined in order.  16 phases instead of 4 keep 4x more loads in
@@ -401,8 +429,9 @@ template <int MODE>
 __global__ void __launch_bounds__(256)
 colsum4_kernel(const float* __restrict__ V, int ld, int C, int R, const float* __restrict__ mean,
                const float* __restrict__ stdv, const float* __restrict__ O, const float* __restrict__ Y,
-               float* __restrict__ part) {
+               float* __restrict__ part, ColFin fin) {
     __shared__ float4 sh[2][16][16];
+    __shared__ int lastf;
     const int tid = threadIdx.x, p = tid >> 4, q = tid & 15, c = blockIdx.y * 64 + 4 * q;
     const int rbeg = blockIdx.x * CS_ROWS, rend = min(R, rbeg + CS_ROWS);
     float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
@@ -441,18 +470,40 @@ colsum4_kernel(const float* __restrict__ V, int ld, int C, int R, const float* _
                 part[((size_t)blockIdx.x * 2 + wch) * C + cc] = a;
             }
         }
+        // release at device scope: the partials leave this XCD's L2 before the block counts in
+        __threadfence();
+    }
+    // The last row block of this channel block to arrive finalizes it (one launch instead of two:
+    // the finalize kernels were 4.8 us each, 172 per training step).  Thread (quarter qq, channel
+    // cl) sums row blocks qq, qq + 4, ... in order, the quarters in order: a fixed order, so the
+    // step stays bit-reproducible.
+    __syncthreads();
+    if (tid == 0) lastf = atomicAdd(fin.ctr + blockIdx.y, 1) == (int)gridDim.x - 1;
+    __syncthreads();
+    if (!lastf) return;
+    __threadfence();                                   // acquire: the other blocks' partials
+    const int cl = tid & 63, qq = tid >> 6, cc = blockIdx.y * 64 + cl, nblk = gridDim.x;
+    float* fsh = reinterpret_cast<float*>(sh);         // [2][4][64] floats, reused
+    float a0 = 0.0f, a1 = 0.0f;
+    if (cc < C) {
+#pragma unroll 4
+        for (int b = qq; b < nblk; b += 4) {
+            a0 += part[((size_t)b * 2) * C + cc];
+            if (MODE == 2) a1 += part[((size_t)b * 2 + 1) * C + cc];
+        }
+    }
+    __syncthreads();                                   // every read of sh above is done
+    fsh[qq * 64 + cl] = a0;
+    fsh[256 + qq * 64 + cl] = a1;
+    __syncthreads();
+    if (tid < 64) {
+        if (cc < C)
+            fin_store(fin, cc, R, ((fsh[cl] + fsh[64 + cl]) + fsh[128 + cl]) + fsh[192 + cl],
+                      ((fsh[256 + cl] + fsh[320 + cl]) + fsh[384 + cl]) + fsh[448 + cl]);
+        if (tid == 0) fin.ctr[blockIdx.y] = 0;         // ready for the next launch on this stream
     }
 }
 
-// colsum with 16-byte loads when the channel layout allows it, else the scalar kernel
-template <int MODE>
-void launch_colsum(dim3 g, hipStream_t st, const float* V, int ld, int C, int R, const float* mean, const float* stdv,
-                   const float* O, const float* Y, float* part) {
-    const bool vec = C % 4 == 0 && ld % 4 == 0 && ((uintptr_t)V & 15) == 0 && (!O || ((uintptr_t)O & 15) == 0) &&
-                     (!Y || ((uintptr_t)Y & 15) == 0);
-    if (vec) colsum4_kernel<MODE><<<g, 256, 0, st>>>(V, ld, C, R, mean, stdv, O, Y, part);
-    else colsum_kernel<MODE><<<g, 256, 0, st>>>(V, ld, C, R, mean, stdv, O, Y, part);
-}
 
 // sum the row-block partials of channel c, one wavefront per channel: lane l adds blocks
 // l, l + 64, ... in order, then a fixed butterfly over the lanes -- a fixed order (the step stays
@@ -508,6 +559,25 @@ __global__ void finalize_bnback_kernel(const float* __restrict__ part, int nblk,
 }
 #undef FIN_CHANNEL
 
+// column sums + finalize: 16-byte loads with the finalize in the last row block when the channel
+// layout allows it, else the scalar kernel and a finalize kernel
+template <int MODE>
+void launch_colsum(dim3 g, hipStream_t st, const float* V, int ld, int C, int R, const float* mean, const float* stdv,
+                   const float* O, const float* Y, float* part, const ColFin& fin) {
+    const bool vec = C % 4 == 0 && ld % 4 == 0 && ((uintptr_t)V & 15) == 0 && (!O || ((uintptr_t)O & 15) == 0) &&
+                     (!Y || ((uintptr_t)Y & 15) == 0);
+    if (vec) {
+        colsum4_kernel<MODE><<<g, 256, 0, st>>>(V, ld, C, R, mean, stdv, O, Y, part, fin);
+        return;
+    }
+    colsum_kernel<MODE><<<g, 256, 0, st>>>(V, ld, C, R, mean, stdv, O, Y, part);
+    const int nb = (int)g.x, fg = finalize_grid(C);
+    if (fin.kind == FIN_SUM) finalize_sum_kernel<<<fg, 256, 0, st>>>(part, nb, C, fin.a);
+    else if (fin.kind == FIN_MEAN) finalize_mean_kernel<<<fg, 256, 0, st>>>(part, nb, C, R, fin.a);
+    else if (fin.kind == FIN_VAR) finalize_var_kernel<<<fg, 256, 0, st>>>(part, nb, C, R, fin.mean, fin.a, fin.b, fin.c);
+    else finalize_bnback_kernel<<<fg, 256, 0, st>>>(part, nb, C, fin.a, fin.b);
+}
+
 // ------------------------------------------------------------------ element-wise
 // out = relu(((y - mean) / std) * gamma + beta [+ res])   (burn BatchNorm::forward_shared + relu)
 __global__ void bn_apply_kernel(const float* __restrict__ Y, int ld, int C, int R, const float* __restrict__ mean,
@@ -520,6 +590,31 @@ __global__ void bn_apply_kernel(const float* __restrict__ Y, int ld, int C, int 
         float v = ((Y[o] - mean[c]) / stdv[c]) * gamma[c] + beta[c];
         if (res) v += res[o];
         out[o] = fmaxf(v, 0.0f);
+    }
+}
+
+// The same four channels per thread (16-byte accesses; C a power of two in [4, 1024], ld and
+// the pointers 16-byte multiples): thread t owns channel quad t % (C / 4) -- its parameters are
+// loaded once -- and rows t / (C / 4) + k (256 / (C / 4)), so no per-element index division (the
+// scalar kernel: 16.2 us at 32768 x 256)
+__global__ void __launch_bounds__(256) bn_apply4_kernel(const float* __restrict__ Y, int ld, int C, int R,
+                                                        const float* __restrict__ mean, const float* __restrict__ stdv,
+                                                        const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                        const float* __restrict__ res, float* __restrict__ out) {
+    const int cq = C / 4, c = 4 * (threadIdx.x % cq), rs = 256 / cq;
+    const float4 mu = *reinterpret_cast<const float4*>(mean + c), sd = *reinterpret_cast<const float4*>(stdv + c);
+    const float4 ga = *reinterpret_cast<const float4*>(gamma + c), be = *reinterpret_cast<const float4*>(beta + c);
+    for (int r = blockIdx.x * rs + (int)threadIdx.x / cq; r < R; r += gridDim.x * rs) {
+        const size_t o = (size_t)r * ld + c;
+        const float4 y = *reinterpret_cast<const float4*>(Y + o);
+        float4 v = make_float4(((y.x - mu.x) / sd.x) * ga.x + be.x, ((y.y - mu.y) / sd.y) * ga.y + be.y,
+                               ((y.z - mu.z) / sd.z) * ga.z + be.z, ((y.w - mu.w) / sd.w) * ga.w + be.w);
+        if (res) {
+            const float4 q = *reinterpret_cast<const float4*>(res + o);
+            v.x += q.x; v.y += q.y; v.z += q.z; v.w += q.w;
+        }
+        *reinterpret_cast<float4*>(out + o) =
+            make_float4(fmaxf(v.x, 0.0f), fmaxf(v.y, 0.0f), fmaxf(v.z, 0.0f), fmaxf(v.w, 0.0f));
     }
 }
 
@@ -538,6 +633,33 @@ __global__ void bn_back_kernel(const float* __restrict__ dout, const float* __re
         const float yhat = (Y[o] - mean[c]) / stdv[c];
         dy[o] = (gamma[c] / stdv[c]) * (dz - dbeta[c] * invR - yhat * dgamma[c] * invR);
         if (dres) dres[o] = dz;
+    }
+}
+
+// bn_back_kernel four channels per thread, laid out as bn_apply4_kernel
+__global__ void __launch_bounds__(256) bn_back4_kernel(const float* __restrict__ dout, const float* __restrict__ O,
+                                                       const float* __restrict__ Y, int ld, int C, int R,
+                                                       const float* __restrict__ mean, const float* __restrict__ stdv,
+                                                       const float* __restrict__ gamma, const float* __restrict__ dgamma,
+                                                       const float* __restrict__ dbeta, float* __restrict__ dy,
+                                                       float* __restrict__ dres) {
+    const int cq = C / 4, c = 4 * (threadIdx.x % cq), rs = 256 / cq;
+    const float invR = 1.0f / (float)R;
+    const float4 mu = *reinterpret_cast<const float4*>(mean + c), sd = *reinterpret_cast<const float4*>(stdv + c);
+    const float4 ga = *reinterpret_cast<const float4*>(gamma + c), dg = *reinterpret_cast<const float4*>(dgamma + c);
+    const float4 db = *reinterpret_cast<const float4*>(dbeta + c);
+    for (int r = blockIdx.x * rs + (int)threadIdx.x / cq; r < R; r += gridDim.x * rs) {
+        const size_t o = (size_t)r * ld + c;
+        const float4 d = *reinterpret_cast<const float4*>(dout + o), ov = *reinterpret_cast<const float4*>(O + o);
+        const float4 y = *reinterpret_cast<const float4*>(Y + o);
+        const float4 dz = make_float4(ov.x > 0.0f ? d.x : 0.0f, ov.y > 0.0f ? d.y : 0.0f, ov.z > 0.0f ? d.z : 0.0f,
+                                      ov.w > 0.0f ? d.w : 0.0f);
+        *reinterpret_cast<float4*>(dy + o) =
+            make_float4((ga.x / sd.x) * (dz.x - db.x * invR - ((y.x - mu.x) / sd.x) * dg.x * invR),
+                        (ga.y / sd.y) * (dz.y - db.y * invR - ((y.y - mu.y) / sd.y) * dg.y * invR),
+                        (ga.z / sd.z) * (dz.z - db.z * invR - ((y.z - mu.z) / sd.z) * dg.z * invR),
+                        (ga.w / sd.w) * (dz.w - db.w * invR - ((y.w - mu.w) / sd.w) * dg.w * invR));
+        if (dres) *reinterpret_cast<float4*>(dres + o) = dz;
     }
 }
 
@@ -704,7 +826,12 @@ __global__ void __launch_bounds__(256) wino_weights_kernel(const float* __restri
     const float* __restrict__ w = w0 + (blockIdx.y >> 1) * wstride;
     float* __restrict__ U = U0 + (size_t)blockIdx.y * ustride;
     if (idx >= F * F) return;
-    const int o = idx / F, i = idx % F;      // output / input channel of the conv U describes
+    // thread -> (output o, input i) in the order of U's innermost dimensions (i % 4, o % 16,
+    // (i % 16) / 4), so that a workgroup's stores of one point are 1 KB contiguous (o = idx / F,
+    // i = idx % F wrote 16-byte pieces 256 B apart: 309 us for the step's 80 transforms); a
+    // workgroup covers a 16 x 16 (o, i) block, whose weight reads are rows of 16 x 9 floats
+    const int blk = idx >> 8, o = (blk % (F / 16)) * 16 + ((idx >> 2) & 15);
+    const int i = (blk / (F / 16)) * 16 + ((idx >> 6) & 3) * 4 + (idx & 3);   // output / input channel of U's conv
     double g[3][3];
     for (int ky = 0; ky < 3; ky++)
         for (int kx = 0; kx < 3; kx++)
@@ -735,86 +862,36 @@ __global__ void repack3x3_kernel(const float* __restrict__ w, int co_n, int ci_n
     }
 }
 
-// Winograd weight grad of a residual conv (F(2x2, 3x3), the forward conv's transforms
-// transposed): with V = B^T d B the input patch transform (as in the forward) and
-// M' = A dY A^T the 4x4 image of the tile's 2x2 output gradient (Y = A^T M A, so dL/dM = A dY A^T),
-//   dU[xi][ci][co] = sum over (board, tile) of V[xi][ci] M'[xi][co]   (16 GEMMs, wgrad_f32_kernel)
-//   dW[co][ci]     = G^T dU[co][ci] G                                   (U = G g G^T)
-// 2.25x fewer MFMAs than the 9-tap implicit GEMM.  Vt[xi][k][ci], Mt[xi][k][co] with
-// k = board * 16 + tile; one thread per (k, channel), channels fastest (coalesced).
-// Round 4: the training step no longer launches this kernel -- wino_wgrad_gemm_kernel computes the
-// same transforms in its staging -- it stays as the reference of tools/wgrad_dbg.hip.
-__global__ void __launch_bounds__(256) wino_wgrad_transform_kernel(const float* __restrict__ X,
-                                                                   const float* __restrict__ DY, int F, int B,
-                                                                   float* __restrict__ Vt, float* __restrict__ Mt) {
-    const size_t K = (size_t)B * 16, n = K * F;
-    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
-        const int c = (int)(e % F);
-        const size_t k = e / F;
-        const int t = (int)(k & 15), ty = t >> 2, tx = t & 3;
-        const size_t b64 = (k >> 4) * 64;
-        float d[4][4];
+// The split reduction and dW = G^T dU G in one pass: dU[xi][e] = sum over splits s (in order) of
+// partial[s][xi][e], e = ci F + co, then dW[co][ci] = G^T dU G in f64, rounded once, into the gradient's burn layout
+// g[co][ci][3][3] (bit-identical to the round-3 reduce_kernel + separate transform: one launch and
+// no dU round trip, 13.4 + 5.7 us per conv before).
+// Workgroup = 64 e (lanes) x 4 waves; wave w sums points 4w .. 4w + 3 (16 independent loads per
+// point in flight), the 16 points meet in LDS, waves 0-2 write kernel row ky = w.
+__global__ void __launch_bounds__(256) wino_wgrad_reduce_out_kernel(const float* __restrict__ partial, int splits,
+                                                                    int F, float* __restrict__ g) {
+    __shared__ double su[16][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const size_t n = (size_t)F * F, e = (size_t)blockIdx.x * 64 + lane;
 #pragma unroll
-        for (int i = 0; i < 4; i++)
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int r = 2 * ty - 1 + i, f = 2 * tx - 1 + j;
-                d[i][j] = ((unsigned)r < 8u && (unsigned)f < 8u) ? X[(b64 + r * 8 + f) * F + c] : 0.0f;
-            }
-        float y[2][2];
-#pragma unroll
-        for (int a = 0; a < 2; a++)
-#pragma unroll
-            for (int bb = 0; bb < 2; bb++) y[a][bb] = DY[(b64 + (2 * ty + a) * 8 + 2 * tx + bb) * F + c];
-        float tt[4][4], p[4][2];
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            tt[0][j] = d[0][j] - d[2][j];
-            tt[1][j] = d[1][j] + d[2][j];
-            tt[2][j] = d[2][j] - d[1][j];
-            tt[3][j] = d[1][j] - d[3][j];
-        }
-#pragma unroll
-        for (int bb = 0; bb < 2; bb++) {
-            p[0][bb] = y[0][bb];
-            p[1][bb] = y[0][bb] + y[1][bb];
-            p[2][bb] = y[0][bb] - y[1][bb];
-            p[3][bb] = -y[1][bb];
-        }
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const float v[4] = {tt[r][0] - tt[r][2], tt[r][1] + tt[r][2], tt[r][2] - tt[r][1], tt[r][1] - tt[r][3]};
-            const float m[4] = {p[r][0], p[r][0] + p[r][1], p[r][0] - p[r][1], -p[r][1]};
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                Vt[((size_t)(r * 4 + q) * K + k) * F + c] = v[q];
-                Mt[((size_t)(r * 4 + q) * K + k) * F + c] = m[q];
-            }
-        }
+    for (int j = 0; j < 4; j++) {
+        const int x = 4 * w + j;
+        float s = 0.0f;
+        for (int k = 0; k < splits; k++) s += partial[((size_t)k * 16 + x) * n + e];
+        su[x][lane] = s;
     }
-}
-
-// dW = G^T dU G (f64, rounded once) into the gradient's burn layout g[co][ci][3][3]
-__global__ void __launch_bounds__(256) wino_wgrad_out_kernel(const float* __restrict__ dU, int F, float* __restrict__ g) {
-    const size_t n = (size_t)F * F;
-    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
-        const int co = (int)(e % F), ci = (int)(e / F);      // dU[xi][ci][co]
-        double u[4][4];
+    __syncthreads();
+    if (w >= 3) return;
+    const int ky = w, co = (int)(e % F), ci = (int)(e / F);
+    const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
+    double tg[4];
 #pragma unroll
-        for (int x = 0; x < 16; x++) u[x >> 2][x & 3] = dU[(size_t)x * n + e];
-        const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
-        double tg[3][4];
+    for (int j = 0; j < 4; j++)
+        tg[j] = G[0][ky] * su[j][lane] + G[1][ky] * su[4 + j][lane] + G[2][ky] * su[8 + j][lane] + G[3][ky] * su[12 + j][lane];
 #pragma unroll
-        for (int ky = 0; ky < 3; ky++)
-#pragma unroll
-            for (int j = 0; j < 4; j++) tg[ky][j] = G[0][ky] * u[0][j] + G[1][ky] * u[1][j] + G[2][ky] * u[2][j] + G[3][ky] * u[3][j];
-#pragma unroll
-        for (int ky = 0; ky < 3; ky++)
-#pragma unroll
-            for (int kx = 0; kx < 3; kx++)
-                g[((size_t)co * F + ci) * 9 + ky * 3 + kx] =
-                    (float)(tg[ky][0] * G[0][kx] + tg[ky][1] * G[1][kx] + tg[ky][2] * G[2][kx] + tg[ky][3] * G[3][kx]);
-    }
+    for (int kx = 0; kx < 3; kx++)
+        g[((size_t)co * F + ci) * 9 + ky * 3 + kx] =
+            (float)(tg[0] * G[0][kx] + tg[1] * G[1][kx] + tg[2] * G[2][kx] + tg[3] * G[3][kx]);
 }
 
 // dWf[t][k][co] -> grad [co][ci][3][3]
@@ -922,7 +999,6 @@ struct Trainer {
     std::vector<float*> uf, ud;              // conv i's forward / data-grad U: ubase + (2 (i - 1) + {0, 1}) ubytes
     float* ubase = nullptr;
     size_t ubytes = 0;
-    float* wdu = nullptr;                    // Winograd weight grad dU [16][F][F]
     float *w40f = nullptr, *w40d = nullptr, *b40 = nullptr, *wp2f = nullptr, *w1d = nullptr;
     // saved activations (R = B*64 rows)
     float* x0 = nullptr;                     // [R][64] input planes
@@ -935,6 +1011,7 @@ struct Trainer {
     float *bmean = nullptr, *bstd = nullptr, *dgb = nullptr;
     // reduction scratch
     float *wpart = nullptr, *cpart = nullptr, *dwtmp = nullptr;
+    int* cctr = nullptr;                     // colsum arrival counters (tr::ColFin)
     size_t wpart_cap = 0, dwtmp_cap = 0;
     int slot = 0;                            // per-BN statistics stride (>= every BN's channels)
     float *tpol = nullptr, *tval = nullptr, *planes = nullptr, *loss = nullptr, *vpart = nullptr;
@@ -1028,13 +1105,26 @@ int launch_wino_wgrad(Trainer* T, const float* X, const float* DY, int B, float*
     if (splits * 16 * (size_t)F * F > T->wpart_cap) return fail("Winograd wgrad: partial buffer too small");
     hipStream_t st = T->st;
     tr::wino_wgrad_gemm_kernel<<<dim3(splits, 16), 512, 0, st>>>(X, DY, K, WINO_GEMM_ROWS, T->wpart);
-    const size_t n = (size_t)16 * F * F;
-    tr::reduce_kernel<<<grid_for(n), 256, 0, st>>>(T->wpart, splits, n, T->wdu);
-    tr::wino_wgrad_out_kernel<<<grid_for((size_t)F * F), 256, 0, st>>>(T->wdu, F, g);
+    if ((size_t)F * F % 64) return fail("Winograd wgrad: F * F must be a multiple of 64");
+    tr::wino_wgrad_reduce_out_kernel<<<(unsigned)((size_t)F * F / 64), 256, 0, st>>>(T->wpart, splits, F, g);
     return hipGetLastError() == hipSuccess ? 0 : fail("Winograd wgrad launch failed");
 }
 
 int nblk_rows(int R) { return (R + tr::CS_ROWS - 1) / tr::CS_ROWS; }
+
+// the four-channel BN kernels apply: C a power of two in [4, 1024], ld and every pointer 16-byte
+// aligned (the per-channel parameter vectors at channel 0 included: c is a multiple of 4)
+bool bn_vec(int C, int ld, std::initializer_list<const float*> ptrs) {
+    if (C < 4 || C > 1024 || (C & (C - 1)) || ld % 4) return false;
+    for (const float* q : ptrs)
+        if (((uintptr_t)q & 15) != 0) return false;
+    return true;
+}
+// rows of 256 / (C / 4) per workgroup step; enough workgroups for 16 waves per CU at most
+unsigned bn_grid(int C, int R) {
+    const int rs = 256 / (C / 4);
+    return (unsigned)std::max(1, std::min((R + rs - 1) / rs, 256 * 4));
+}
 
 // BatchNorm (training) + ReLU (+ residual): Y -> out; saves mean/std in slot `bi`
 int bn_forward(Trainer* T, int bi, const float* Y, int ld, int C, int R, size_t bn_off, const float* res, float* out) {
@@ -1044,11 +1134,14 @@ int bn_forward(Trainer* T, int bi, const float* Y, int ld, int C, int R, size_t 
     float* sd = T->bstd + (size_t)bi * T->slot;
     const int nb = nblk_rows(R);
     dim3 g(nb, (C + 63) / 64);
-    tr::launch_colsum<0>(g, T->st, Y, ld, C, R, nullptr, nullptr, nullptr, nullptr, T->cpart);
-    tr::finalize_mean_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(T->cpart, nb, C, R, mean);
-    tr::launch_colsum<1>(g, T->st, Y, ld, C, R, mean, nullptr, nullptr, nullptr, T->cpart);
-    tr::finalize_var_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(T->cpart, nb, C, R, mean, sd, P + 2 * C, P + 3 * C);
-    tr::bn_apply_kernel<<<grid_for((size_t)R * C), 256, 0, T->st>>>(Y, ld, C, R, mean, sd, P, P + C, res, out);
+    tr::launch_colsum<0>(g, T->st, Y, ld, C, R, nullptr, nullptr, nullptr, nullptr, T->cpart,
+                         {tr::FIN_MEAN, mean, nullptr, nullptr, nullptr, T->cctr});
+    tr::launch_colsum<1>(g, T->st, Y, ld, C, R, mean, nullptr, nullptr, nullptr, T->cpart,
+                         {tr::FIN_VAR, sd, P + 2 * C, P + 3 * C, mean, T->cctr});
+    if (bn_vec(C, ld, {Y, res, out, P, mean, sd}))
+        tr::bn_apply4_kernel<<<bn_grid(C, R), 256, 0, T->st>>>(Y, ld, C, R, mean, sd, P, P + C, res, out);
+    else
+        tr::bn_apply_kernel<<<grid_for((size_t)R * C), 256, 0, T->st>>>(Y, ld, C, R, mean, sd, P, P + C, res, out);
     return hipGetLastError() == hipSuccess ? 0 : fail("bn forward failed");
 }
 
@@ -1059,20 +1152,24 @@ int bn_backward(Trainer* T, int bi, const float* dout, const float* O, const flo
     const float* sd = T->bstd + (size_t)bi * T->slot;
     const int nb = nblk_rows(R);
     dim3 g(nb, (C + 63) / 64);
-    tr::launch_colsum<2>(g, T->st, dout, ld, C, R, mean, sd, O, Y, T->cpart);
     float* dgam = T->g + bn_off;
     float* dbet = T->g + bn_off + C;
-    tr::finalize_bnback_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(T->cpart, nb, C, dgam, dbet);
-    tr::bn_back_kernel<<<grid_for((size_t)R * C), 256, 0, T->st>>>(dout, O, Y, ld, C, R, mean, sd, T->p + bn_off, dgam,
-                                                                   dbet, dy, dres);
+    tr::launch_colsum<2>(g, T->st, dout, ld, C, R, mean, sd, O, Y, T->cpart,
+                         {tr::FIN_BNBACK, dgam, dbet, nullptr, nullptr, T->cctr});
+    if (bn_vec(C, ld, {dout, O, Y, dy, dres, T->p + bn_off, dgam, mean, sd}))
+        tr::bn_back4_kernel<<<bn_grid(C, R), 256, 0, T->st>>>(dout, O, Y, ld, C, R, mean, sd, T->p + bn_off, dgam, dbet,
+                                                              dy, dres);
+    else
+        tr::bn_back_kernel<<<grid_for((size_t)R * C), 256, 0, T->st>>>(dout, O, Y, ld, C, R, mean, sd, T->p + bn_off,
+                                                                       dgam, dbet, dy, dres);
     return hipGetLastError() == hipSuccess ? 0 : fail("bn backward failed");
 }
 
 int bias_grad(Trainer* T, const float* dy, int ld, int C, int R, float* dst) {
     const int nb = nblk_rows(R);
     dim3 g(nb, (C + 63) / 64);
-    tr::launch_colsum<0>(g, T->st, dy, ld, C, R, nullptr, nullptr, nullptr, nullptr, T->cpart);
-    tr::finalize_sum_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(T->cpart, nb, C, dst);
+    tr::launch_colsum<0>(g, T->st, dy, ld, C, R, nullptr, nullptr, nullptr, nullptr, T->cpart,
+                         {tr::FIN_SUM, dst, nullptr, nullptr, nullptr, T->cctr});
     return hipGetLastError() == hipSuccess ? 0 : fail("bias grad failed");
 }
 
@@ -1093,6 +1190,7 @@ int trainer_grads(Trainer* T, const float* planes, const float* tpol, const floa
     // weights of this step in GEMM layouts
     if (T->wino && T->blocks > 0) {  // residual convs: Winograd weights, forward and data grad, one launch
         const size_t wstride = L.tower.size() > 2 ? L.tower[2].w - L.tower[1].w : 0;
+        if (F % 16) return fail("train: Winograd weights need F % 16 == 0");
         tr::wino_weights_kernel<<<dim3((unsigned)((F * F + 255) / 256), 2 * (L.tower.size() - 1)), 256, 0, st>>>(
             T->p + L.tower[1].w, wstride, F, T->ubase, T->ubytes / sizeof(float));
     }
@@ -1349,11 +1447,11 @@ int az_trainer_create(int blocks, int filters, const float* weights, size_t n, i
     wp = std::max(wp, sl * 512 * 64);                                   // value_linear_1
     if (T->wino) {   // Winograd weight grads: [16][Bmax * 16][F] transforms, dU [16][F][F]
         wp = std::max(wp, wino_gemm_splits(max_batch) * 16 * (size_t)F * F);
-        T->wdu = A((size_t)16 * F * F);
     }
     T->wpart = A(wp);
     T->wpart_cap = wp;
     T->cpart = A((R / tr::CS_ROWS + 2) * 2 * (size_t)std::max(F, 65));
+    T->cctr = reinterpret_cast<int*>(A(64));
     // dW scratch: input conv [9][64][F], residual conv [9][F][F], heads [F][64] + its [40][F]
     // transpose, policy_conv_2 [32][64], value_linear_2 partial sums (65)
     T->dwtmp_cap = std::max({(size_t)9 * 64 * F, (size_t)9 * F * F, (size_t)F * 64 + 40 * (size_t)F, (size_t)32 * 64,
@@ -1385,7 +1483,8 @@ int az_trainer_create(int blocks, int filters, const float* weights, size_t n, i
         return fail("az_trainer_create: upload failed");
     }
     // the Winograd weight buffers' prefetch pad stays zero (the per-step transforms write the rest)
-    if (T->ubase && hipMemset(T->ubase, 0, 2 * (size_t)(nconv - 1) * T->ubytes) != hipSuccess) {
+    if ((T->ubase && hipMemset(T->ubase, 0, 2 * (size_t)(nconv - 1) * T->ubytes) != hipSuccess) ||
+        hipMemset(T->cctr, 0, 64 * sizeof(int)) != hipSuccess) {
         delete T;
         return fail("az_trainer_create: upload failed");
     }

@@ -35,7 +35,7 @@ PEAK_HBM_GBS = 8000.0         # MI355X_MICROARCH.md: 8.0 TB/s spec
 # gfx950 correction + WRITE_SIZE), same kernel and per-launch work (2048 rows, 20x256)
 PMC_SUMMARY = {"f32": os.path.join(ROOT, "profiles", "r03_pmc_tower32w_8_summary.json"),           # Winograd
                "f32-direct": os.path.join(ROOT, "profiles", "r02_pmc_tower32_summary.json"),      # AZ_WINOGRAD=0
-               "bf16": os.path.join(ROOT, "profiles", "r01_pmc_tower_v11_summary.json")}
+               "bf16": os.path.join(ROOT, "profiles", "r04_pmc_tower_bf16_summary.json")}
 # simulation steps of the instrumented profile pass after the timed window (8 sampled tower launches)
 PROFILE_SIMS = 256
 # mean plies of complete self-play games of this config (tools/game_length.py: 256 games, 20x256

@@ -1,11 +1,74 @@
-// wgrad_dbg.hip -- debug harness for the fused-transform Winograd weight grad (tools/wgrad_fused.patch):
-// the patch's kernel, standalone, with its first stage's LDS image (xs = V rows, ds = M' rows) dumped
+// wgrad_dbg.hip -- debug harness for the fused-transform Winograd weight grad (wino_wgrad_gemm_kernel):
+// the kernel, standalone, with its first stage's LDS image (xs = V rows, ds = M' rows) dumped
 // after the staging barrier, against wino_wgrad_transform_kernel's Vt / Mt for the same board; then the
 // whole partial against a host GEMM of Vt x Mt.  Splits "gather wrong" from "GEMM wrong" in one run.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -o tools/wgrad_dbg tools/wgrad_dbg.hip -lrccl
 #include "../alphazero-chess_amd/csrc/train.hip"
 #include <cstdio>
 #include <vector>
+
+namespace azi {
+namespace tr {
+// Winograd weight grad of a residual conv (F(2x2, 3x3), the forward conv's transforms
+// transposed): with V = B^T d B the input patch transform (as in the forward) and
+// M' = A dY A^T the 4x4 image of the tile's 2x2 output gradient (Y = A^T M A, so dL/dM = A dY A^T),
+//   dU[xi][ci][co] = sum over (board, tile) of V[xi][ci] M'[xi][co]   (16 GEMMs, wgrad_f32_kernel)
+//   dW[co][ci]     = G^T dU[co][ci] G                                   (U = G g G^T)
+// 2.25x fewer MFMAs than the 9-tap implicit GEMM.  Vt[xi][k][ci], Mt[xi][k][co] with
+// k = board * 16 + tile; one thread per (k, channel), channels fastest (coalesced).
+// (The round-3 training step's transform pass; wino_wgrad_gemm_kernel now computes the same
+// transforms in its staging, and this is the reference it is checked against.)
+__global__ void __launch_bounds__(256) wino_wgrad_transform_kernel(const float* __restrict__ X,
+                                                                   const float* __restrict__ DY, int F, int B,
+                                                                   float* __restrict__ Vt, float* __restrict__ Mt) {
+    const size_t K = (size_t)B * 16, n = K * F;
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
+        const int c = (int)(e % F);
+        const size_t k = e / F;
+        const int t = (int)(k & 15), ty = t >> 2, tx = t & 3;
+        const size_t b64 = (k >> 4) * 64;
+        float d[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int r = 2 * ty - 1 + i, f = 2 * tx - 1 + j;
+                d[i][j] = ((unsigned)r < 8u && (unsigned)f < 8u) ? X[(b64 + r * 8 + f) * F + c] : 0.0f;
+            }
+        float y[2][2];
+#pragma unroll
+        for (int a = 0; a < 2; a++)
+#pragma unroll
+            for (int bb = 0; bb < 2; bb++) y[a][bb] = DY[(b64 + (2 * ty + a) * 8 + 2 * tx + bb) * F + c];
+        float tt[4][4], p[4][2];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            tt[0][j] = d[0][j] - d[2][j];
+            tt[1][j] = d[1][j] + d[2][j];
+            tt[2][j] = d[2][j] - d[1][j];
+            tt[3][j] = d[1][j] - d[3][j];
+        }
+#pragma unroll
+        for (int bb = 0; bb < 2; bb++) {
+            p[0][bb] = y[0][bb];
+            p[1][bb] = y[0][bb] + y[1][bb];
+            p[2][bb] = y[0][bb] - y[1][bb];
+            p[3][bb] = -y[1][bb];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const float v[4] = {tt[r][0] - tt[r][2], tt[r][1] + tt[r][2], tt[r][2] - tt[r][1], tt[r][1] - tt[r][3]};
+            const float m[4] = {p[r][0], p[r][0] + p[r][1], p[r][0] - p[r][1], -p[r][1]};
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                Vt[((size_t)(r * 4 + q) * K + k) * F + c] = v[q];
+                Mt[((size_t)(r * 4 + q) * K + k) * F + c] = m[q];
+            }
+        }
+    }
+}
+}  // namespace tr
+}  // namespace azi
 
 // the library entry points train.hip refers to (not exercised here)
 namespace azi { int fail(const std::string& m) { fprintf(stderr, "%s\n", m.c_str()); return -1; } }
