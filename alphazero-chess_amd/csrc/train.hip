@@ -241,7 +241,8 @@ wgrad_f32_kernel(const float* __restrict__ X, int ldx, int K, const float* __res
 // GEMM: 8 waves, wave w owns co [32 w, 32 w + 32) x all 256 ci: accumulator block (j, c) row m is
 // ci = 64 j + 4 m + c, so one ds_read_b128 of a row feeds four blocks.  The next board's squares
 // are loaded into registers beside the current board's MFMAs.  partial[split][xi][ci][co]; every
-// element sums its split's rows in row order (fixed order; splits reduced in order by reduce_kernel).
+// element sums its split's rows in row order (fixed order; splits reduced in order by
+// wino_wgrad_reduce_out_kernel).
 constexpr int WG_S = 256 + 16;
 // the four F(2x2,3x3) combinations: (a, b) = (e0, e2) / (e1, e2) / (e1, e2) / (e1, e3) of a patch
 // row or column -> a - b, a + b, b - a, a - b (B^T rows)
@@ -250,8 +251,12 @@ __global__ void __launch_bounds__(512)
 wino_wgrad_gemm_kernel(const float* __restrict__ X, const float* __restrict__ DY, int K, int rows_per_split,
                        float* __restrict__ partial) {
     constexpr int F = 256;
-    __shared__ __attribute__((aligned(16))) float xs[16 * WG_S];
-    __shared__ __attribute__((aligned(16))) float ds[16 * WG_S];
+    // two stages of V / M' rows: the transform of board s + 1 goes into the other buffer right
+    // after this wave's MFMAs of board s, so one barrier per board and a wave that finishes its
+    // MFMAs early transforms beside the others' (single-buffered: two barriers per board and the
+    // transform with no MFMA beside it, 179 us per launch at B = 512)
+    __shared__ __attribute__((aligned(16))) float xs[2][16 * WG_S];
+    __shared__ __attribute__((aligned(16))) float ds[2][16 * WG_S];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int split = blockIdx.x, xi = blockIdx.y, r = xi >> 2, q = xi & 3;
     const int i1 = r == 0 ? 0 : 1, i2 = r == 3 ? 3 : 2, j1 = q == 0 ? 0 : 1, j2 = q == 3 ? 3 : 2;
@@ -285,9 +290,7 @@ wino_wgrad_gemm_kernel(const float* __restrict__ X, const float* __restrict__ DY
                     yv[u][a][bb] = *reinterpret_cast<const f32x4*>(DY + (b64 + (2 * ty + a) * 8 + 2 * tx + bb) * F + c4);
         }
     };
-    if (rbeg < rend) fetch(rbeg);
-    for (int rc = rbeg; rc < rend; rc += 16) {
-        __syncthreads();
+    auto stage = [&](int buf) {
 #pragma unroll
         for (int u = 0; u < 2; u++) {
             const int t = 2 * tp + u;
@@ -305,19 +308,28 @@ wino_wgrad_gemm_kernel(const float* __restrict__ X, const float* __restrict__ DY
 #pragma unroll
             for (int bb = 0; bb < 2; bb++) p[bb] = yv[u][0][bb] * ra + yv[u][1][bb] * rb;
             const f32x4 m = p[0] * qa + p[1] * qb;
-            *reinterpret_cast<f32x4*>(xs + t * WG_S + c4) = v;
-            *reinterpret_cast<f32x4*>(ds + t * WG_S + c4) = m;
+            *reinterpret_cast<f32x4*>(xs[buf] + t * WG_S + c4) = v;
+            *reinterpret_cast<f32x4*>(ds[buf] + t * WG_S + c4) = m;
         }
-        __syncthreads();
-        if (rc + 16 < rend) fetch(rc + 16);
+    };
+    if (rbeg < rend) {
+        fetch(rbeg);
+        stage(0);
+    }
+    __syncthreads();
+    for (int rc = rbeg, buf = 0; rc < rend; rc += 16, buf ^= 1) {
+        const bool more = rc + 16 < rend;
+        if (more) fetch(rc + 16);
+        const float* xb = xs[buf];
+        const float* db = ds[buf];
 #pragma unroll
         for (int qq = 0; qq < 4; qq++) {
             const int rq = qq * 4 + (lane >> 4);
-            const float b0 = ds[rq * WG_S + 32 * w + (lane & 15)];
-            const float b1 = ds[rq * WG_S + 32 * w + 16 + (lane & 15)];
+            const float b0 = db[rq * WG_S + 32 * w + (lane & 15)];
+            const float b1 = db[rq * WG_S + 32 * w + 16 + (lane & 15)];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                const f32x4 a = *reinterpret_cast<const f32x4*>(xs + rq * WG_S + 64 * j + 4 * (lane & 15));
+                const f32x4 a = *reinterpret_cast<const f32x4*>(xb + rq * WG_S + 64 * j + 4 * (lane & 15));
 #pragma unroll
                 for (int c = 0; c < 4; c++) {
                     acc[4 * j + c][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c], b0, acc[4 * j + c][0], 0, 0, 0);
@@ -325,6 +337,10 @@ wino_wgrad_gemm_kernel(const float* __restrict__ X, const float* __restrict__ DY
                 }
             }
         }
+        // the other buffer was last read in the previous board's MFMAs, before the barrier below
+        // ended that iteration
+        if (more) stage(buf ^ 1);
+        __syncthreads();
     }
     float* out = partial + ((size_t)split * 16 + xi) * F * F;
 #pragma unroll
