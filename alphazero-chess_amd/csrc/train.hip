@@ -251,12 +251,8 @@ __global__ void __launch_bounds__(512)
 wino_wgrad_gemm_kernel(const float* __restrict__ X, const float* __restrict__ DY, int K, int rows_per_split,
                        float* __restrict__ partial) {
     constexpr int F = 256;
-    // two stages of V / M' rows: the transform of board s + 1 goes into the other buffer right
-    // after this wave's MFMAs of board s, so one barrier per board and a wave that finishes its
-    // MFMAs early transforms beside the others' (single-buffered: two barriers per board and the
-    // transform with no MFMA beside it, 179 us per launch at B = 512)
-    __shared__ __attribute__((aligned(16))) float xs[2][16 * WG_S];
-    __shared__ __attribute__((aligned(16))) float ds[2][16 * WG_S];
+    __shared__ __attribute__((aligned(16))) float xs[16 * WG_S];
+    __shared__ __attribute__((aligned(16))) float ds[16 * WG_S];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int split = blockIdx.x, xi = blockIdx.y, r = xi >> 2, q = xi & 3;
     const int i1 = r == 0 ? 0 : 1, i2 = r == 3 ? 3 : 2, j1 = q == 0 ? 0 : 1, j2 = q == 3 ? 3 : 2;
@@ -290,7 +286,9 @@ wino_wgrad_gemm_kernel(const float* __restrict__ X, const float* __restrict__ DY
                     yv[u][a][bb] = *reinterpret_cast<const f32x4*>(DY + (b64 + (2 * ty + a) * 8 + 2 * tx + bb) * F + c4);
         }
     };
-    auto stage = [&](int buf) {
+    if (rbeg < rend) fetch(rbeg);
+    for (int rc = rbeg; rc < rend; rc += 16) {
+        __syncthreads();
 #pragma unroll
         for (int u = 0; u < 2; u++) {
             const int t = 2 * tp + u;
@@ -308,28 +306,19 @@ wino_wgrad_gemm_kernel(const float* __restrict__ X, const float* __restrict__ DY
 #pragma unroll
             for (int bb = 0; bb < 2; bb++) p[bb] = yv[u][0][bb] * ra + yv[u][1][bb] * rb;
             const f32x4 m = p[0] * qa + p[1] * qb;
-            *reinterpret_cast<f32x4*>(xs[buf] + t * WG_S + c4) = v;
-            *reinterpret_cast<f32x4*>(ds[buf] + t * WG_S + c4) = m;
+            *reinterpret_cast<f32x4*>(xs + t * WG_S + c4) = v;
+            *reinterpret_cast<f32x4*>(ds + t * WG_S + c4) = m;
         }
-    };
-    if (rbeg < rend) {
-        fetch(rbeg);
-        stage(0);
-    }
-    __syncthreads();
-    for (int rc = rbeg, buf = 0; rc < rend; rc += 16, buf ^= 1) {
-        const bool more = rc + 16 < rend;
-        if (more) fetch(rc + 16);
-        const float* xb = xs[buf];
-        const float* db = ds[buf];
+        __syncthreads();
+        if (rc + 16 < rend) fetch(rc + 16);
 #pragma unroll
         for (int qq = 0; qq < 4; qq++) {
             const int rq = qq * 4 + (lane >> 4);
-            const float b0 = db[rq * WG_S + 32 * w + (lane & 15)];
-            const float b1 = db[rq * WG_S + 32 * w + 16 + (lane & 15)];
+            const float b0 = ds[rq * WG_S + 32 * w + (lane & 15)];
+            const float b1 = ds[rq * WG_S + 32 * w + 16 + (lane & 15)];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                const f32x4 a = *reinterpret_cast<const f32x4*>(xb + rq * WG_S + 64 * j + 4 * (lane & 15));
+                const f32x4 a = *reinterpret_cast<const f32x4*>(xs + rq * WG_S + 64 * j + 4 * (lane & 15));
 #pragma unroll
                 for (int c = 0; c < 4; c++) {
                     acc[4 * j + c][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c], b0, acc[4 * j + c][0], 0, 0, 0);
@@ -337,10 +326,6 @@ wino_wgrad_gemm_kernel(const float* __restrict__ X, const float* __restrict__ DY
                 }
             }
         }
-        // the other buffer was last read in the previous board's MFMAs, before the barrier below
-        // ended that iteration
-        if (more) stage(buf ^ 1);
-        __syncthreads();
     }
     float* out = partial + ((size_t)split * 16 + xi) * F * F;
 #pragma unroll
@@ -371,7 +356,7 @@ __global__ void reduce_kernel(const float* __restrict__ partial, int splits, siz
 //   MODE 0: sum v                       (bias grads, BN mean)
 //   MODE 1: sum (v - mean)^2            (BN biased variance, two-pass like burn)
 //   MODE 2: sum dz, sum dz*yhat with dz = dout*(o > 0), yhat = (y - mean)/std   (BN backward)
-constexpr int CS_ROWS = 128;   // rows per block (256: 8 waves per CU at 32768 rows, colsum4<2> 24 us)
+constexpr int CS_ROWS = 256;   // rows per block
 
 template <int MODE>
 __global__ void __launch_bounds__(256)
@@ -410,32 +395,15 @@ colsum_kernel(const float* __restrict__ V, int ld, int C, int R, const float* __
     }
 }
 
-// What becomes of a column sum once all row blocks are in (the finalize kernels below, or the
-// colsum4 kernel's last block):  SUM a = s0;  MEAN a = s0 / R;  VAR var = s0 / R, a = sqrt(var +
-// eps), b = running mean, c = running var (momentum 0.1, batch mean `mean`);  BNBACK a = dgamma =
-// s1, b = dbeta = s0.  ctr: one arrival counter per 64-channel block, zero between launches.
+// What becomes of a column sum (the finalize kernels below):  SUM a = s0;  MEAN a = s0 / R;  VAR
+// var = s0 / R, a = sqrt(var + eps), b = running mean, c = running var (momentum 0.1, batch mean
+// `mean`);  BNBACK a = dgamma = s1, b = dbeta = s0.
 enum { FIN_SUM, FIN_MEAN, FIN_VAR, FIN_BNBACK };
 struct ColFin {
     int kind;
     float *a, *b, *c;
     const float* mean;
-    int* ctr;
 };
-__device__ __forceinline__ void fin_store(const ColFin& f, int c, int R, float s0, float s1) {
-    if (f.kind == FIN_SUM) {
-        f.a[c] = s0;
-    } else if (f.kind == FIN_MEAN) {
-        f.a[c] = s0 / (float)R;
-    } else if (f.kind == FIN_VAR) {
-        const float var = s0 / (float)R;
-        f.a[c] = sqrtf(var + 1e-5f);
-        f.b[c] = f.b[c] * 0.9f + f.mean[c] * 0.1f;
-        f.c[c] = f.c[c] * 0.9f + var * 0.1f;
-    } else {
-        f.a[c] = s1;
-        f.b[c] = s0;
-    }
-}
 
 // The same sums four channels per thread (16-byte loads; C and ld multiples of 4): thread
 // (phase p = tid / 16, quad q = tid % 16) sums rows rbeg + p, rbeg + p + 16, ... of channels
@@ -445,9 +413,8 @@ template <int MODE>
 __global__ void __launch_bounds__(256)
 colsum4_kernel(const float* __restrict__ V, int ld, int C, int R, const float* __restrict__ mean,
                const float* __restrict__ stdv, const float* __restrict__ O, const float* __restrict__ Y,
-               float* __restrict__ part, ColFin fin) {
+               float* __restrict__ part) {
     __shared__ float4 sh[2][16][16];
-    __shared__ int lastf;
     const int tid = threadIdx.x, p = tid >> 4, q = tid & 15, c = blockIdx.y * 64 + 4 * q;
     const int rbeg = blockIdx.x * CS_ROWS, rend = min(R, rbeg + CS_ROWS);
     float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
@@ -486,37 +453,6 @@ colsum4_kernel(const float* __restrict__ V, int ld, int C, int R, const float* _
                 part[((size_t)blockIdx.x * 2 + wch) * C + cc] = a;
             }
         }
-        // release at device scope: the partials leave this XCD's L2 before the block counts in
-        __threadfence();
-    }
-    // The last row block of this channel block to arrive finalizes it (one launch instead of two:
-    // the finalize kernels were 4.8 us each, 172 per training step).  Thread (quarter qq, channel
-    // cl) sums row blocks qq, qq + 4, ... in order, the quarters in order: a fixed order, so the
-    // step stays bit-reproducible.
-    __syncthreads();
-    if (tid == 0) lastf = atomicAdd(fin.ctr + blockIdx.y, 1) == (int)gridDim.x - 1;
-    __syncthreads();
-    if (!lastf) return;
-    __threadfence();                                   // acquire: the other blocks' partials
-    const int cl = tid & 63, qq = tid >> 6, cc = blockIdx.y * 64 + cl, nblk = gridDim.x;
-    float* fsh = reinterpret_cast<float*>(sh);         // [2][4][64] floats, reused
-    float a0 = 0.0f, a1 = 0.0f;
-    if (cc < C) {
-#pragma unroll 4
-        for (int b = qq; b < nblk; b += 4) {
-            a0 += part[((size_t)b * 2) * C + cc];
-            if (MODE == 2) a1 += part[((size_t)b * 2 + 1) * C + cc];
-        }
-    }
-    __syncthreads();                                   // every read of sh above is done
-    fsh[qq * 64 + cl] = a0;
-    fsh[256 + qq * 64 + cl] = a1;
-    __syncthreads();
-    if (tid < 64) {
-        if (cc < C)
-            fin_store(fin, cc, R, ((fsh[cl] + fsh[64 + cl]) + fsh[128 + cl]) + fsh[192 + cl],
-                      ((fsh[256 + cl] + fsh[320 + cl]) + fsh[384 + cl]) + fsh[448 + cl]);
-        if (tid == 0) fin.ctr[blockIdx.y] = 0;         // ready for the next launch on this stream
     }
 }
 
@@ -575,18 +511,17 @@ __global__ void finalize_bnback_kernel(const float* __restrict__ part, int nblk,
 }
 #undef FIN_CHANNEL
 
-// column sums + finalize: 16-byte loads with the finalize in the last row block when the channel
-// layout allows it, else the scalar kernel and a finalize kernel
+// column sums (16-byte loads when the channel layout allows it, else the scalar kernel), then the
+// finalize kernel of `fin`.  (Finalizing in the last row block to arrive instead -- an arrival
+// counter and device-scope fences -- measured 6.4 -> 38.7 us for the MODE 0 sums: each block's
+// release fence writes back its XCD's L2, dirty with the previous kernel's output.)
 template <int MODE>
 void launch_colsum(dim3 g, hipStream_t st, const float* V, int ld, int C, int R, const float* mean, const float* stdv,
                    const float* O, const float* Y, float* part, const ColFin& fin) {
     const bool vec = C % 4 == 0 && ld % 4 == 0 && ((uintptr_t)V & 15) == 0 && (!O || ((uintptr_t)O & 15) == 0) &&
                      (!Y || ((uintptr_t)Y & 15) == 0);
-    if (vec) {
-        colsum4_kernel<MODE><<<g, 256, 0, st>>>(V, ld, C, R, mean, stdv, O, Y, part, fin);
-        return;
-    }
-    colsum_kernel<MODE><<<g, 256, 0, st>>>(V, ld, C, R, mean, stdv, O, Y, part);
+    if (vec) colsum4_kernel<MODE><<<g, 256, 0, st>>>(V, ld, C, R, mean, stdv, O, Y, part);
+    else colsum_kernel<MODE><<<g, 256, 0, st>>>(V, ld, C, R, mean, stdv, O, Y, part);
     const int nb = (int)g.x, fg = finalize_grid(C);
     if (fin.kind == FIN_SUM) finalize_sum_kernel<<<fg, 256, 0, st>>>(part, nb, C, fin.a);
     else if (fin.kind == FIN_MEAN) finalize_mean_kernel<<<fg, 256, 0, st>>>(part, nb, C, R, fin.a);
@@ -879,23 +814,19 @@ __global__ void repack3x3_kernel(const float* __restrict__ w, int co_n, int ci_n
 }
 
 // The split reduction and dW = G^T dU G in one pass: dU[xi][e] = sum over splits s (in order) of
-// partial[s][xi][e], e = ci F + co, then dW[co][ci] = G^T dU G in f64, rounded once, into the gradient's burn layout
-// g[co][ci][3][3] (bit-identical to the round-3 reduce_kernel + separate transform: one launch and
-// no dU round trip, 13.4 + 5.7 us per conv before).
-// Workgroup = 64 e (lanes) x 4 waves; wave w sums points 4w .. 4w + 3 (16 independent loads per
-// point in flight), the 16 points meet in LDS, waves 0-2 write kernel row ky = w.
-__global__ void __launch_bounds__(256) wino_wgrad_reduce_out_kernel(const float* __restrict__ partial, int splits,
-                                                                    int F, float* __restrict__ g) {
-    __shared__ double su[16][64];
+// partial[s][xi][e], e = ci F + co, then dW[co][ci] = G^T dU G in f64, rounded once, into the
+// gradient's burn layout g[co][ci][3][3] (bit-identical to the round-3 reduce_kernel + separate
+// transform, 13.4 + 5.7 us per conv, without the dU round trip).  Workgroup = 64 e (lanes) x 16
+// waves, wave = point xi: each thread's 16 split loads are independent (4 points per wave
+// measured 23.2 us: too few loads in flight), the points meet in LDS, waves 0-2 write kernel row ky.
+__global__ void __launch_bounds__(1024) wino_wgrad_reduce_out_kernel(const float* __restrict__ partial, int splits,
+                                                                     int F, float* __restrict__ g) {
+    __shared__ float su[16][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const size_t n = (size_t)F * F, e = (size_t)blockIdx.x * 64 + lane;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const int x = 4 * w + j;
-        float s = 0.0f;
-        for (int k = 0; k < splits; k++) s += partial[((size_t)k * 16 + x) * n + e];
-        su[x][lane] = s;
-    }
+    float s = 0.0f;
+    for (int k = 0; k < splits; k++) s += partial[((size_t)k * 16 + w) * n + e];
+    su[w][lane] = s;
     __syncthreads();
     if (w >= 3) return;
     const int ky = w, co = (int)(e % F), ci = (int)(e / F);
@@ -903,7 +834,8 @@ __global__ void __launch_bounds__(256) wino_wgrad_reduce_out_kernel(const float*
     double tg[4];
 #pragma unroll
     for (int j = 0; j < 4; j++)
-        tg[j] = G[0][ky] * su[j][lane] + G[1][ky] * su[4 + j][lane] + G[2][ky] * su[8 + j][lane] + G[3][ky] * su[12 + j][lane];
+        tg[j] = G[0][ky] * (double)su[j][lane] + G[1][ky] * (double)su[4 + j][lane] + G[2][ky] * (double)su[8 + j][lane] +
+                G[3][ky] * (double)su[12 + j][lane];
 #pragma unroll
     for (int kx = 0; kx < 3; kx++)
         g[((size_t)co * F + ci) * 9 + ky * 3 + kx] =
@@ -1027,7 +959,6 @@ struct Trainer {
     float *bmean = nullptr, *bstd = nullptr, *dgb = nullptr;
     // reduction scratch
     float *wpart = nullptr, *cpart = nullptr, *dwtmp = nullptr;
-    int* cctr = nullptr;                     // colsum arrival counters (tr::ColFin)
     size_t wpart_cap = 0, dwtmp_cap = 0;
     int slot = 0;                            // per-BN statistics stride (>= every BN's channels)
     float *tpol = nullptr, *tval = nullptr, *planes = nullptr, *loss = nullptr, *vpart = nullptr;
@@ -1122,7 +1053,7 @@ int launch_wino_wgrad(Trainer* T, const float* X, const float* DY, int B, float*
     hipStream_t st = T->st;
     tr::wino_wgrad_gemm_kernel<<<dim3(splits, 16), 512, 0, st>>>(X, DY, K, WINO_GEMM_ROWS, T->wpart);
     if ((size_t)F * F % 64) return fail("Winograd wgrad: F * F must be a multiple of 64");
-    tr::wino_wgrad_reduce_out_kernel<<<(unsigned)((size_t)F * F / 64), 256, 0, st>>>(T->wpart, splits, F, g);
+    tr::wino_wgrad_reduce_out_kernel<<<(unsigned)((size_t)F * F / 64), 1024, 0, st>>>(T->wpart, splits, F, g);
     return hipGetLastError() == hipSuccess ? 0 : fail("Winograd wgrad launch failed");
 }
 
@@ -1151,9 +1082,9 @@ int bn_forward(Trainer* T, int bi, const float* Y, int ld, int C, int R, size_t 
     const int nb = nblk_rows(R);
     dim3 g(nb, (C + 63) / 64);
     tr::launch_colsum<0>(g, T->st, Y, ld, C, R, nullptr, nullptr, nullptr, nullptr, T->cpart,
-                         {tr::FIN_MEAN, mean, nullptr, nullptr, nullptr, T->cctr});
+                         {tr::FIN_MEAN, mean, nullptr, nullptr, nullptr});
     tr::launch_colsum<1>(g, T->st, Y, ld, C, R, mean, nullptr, nullptr, nullptr, T->cpart,
-                         {tr::FIN_VAR, sd, P + 2 * C, P + 3 * C, mean, T->cctr});
+                         {tr::FIN_VAR, sd, P + 2 * C, P + 3 * C, mean});
     if (bn_vec(C, ld, {Y, res, out, P, mean, sd}))
         tr::bn_apply4_kernel<<<bn_grid(C, R), 256, 0, T->st>>>(Y, ld, C, R, mean, sd, P, P + C, res, out);
     else
@@ -1171,7 +1102,7 @@ int bn_backward(Trainer* T, int bi, const float* dout, const float* O, const flo
     float* dgam = T->g + bn_off;
     float* dbet = T->g + bn_off + C;
     tr::launch_colsum<2>(g, T->st, dout, ld, C, R, mean, sd, O, Y, T->cpart,
-                         {tr::FIN_BNBACK, dgam, dbet, nullptr, nullptr, T->cctr});
+                         {tr::FIN_BNBACK, dgam, dbet, nullptr, nullptr});
     if (bn_vec(C, ld, {dout, O, Y, dy, dres, T->p + bn_off, dgam, mean, sd}))
         tr::bn_back4_kernel<<<bn_grid(C, R), 256, 0, T->st>>>(dout, O, Y, ld, C, R, mean, sd, T->p + bn_off, dgam, dbet,
                                                               dy, dres);
@@ -1185,7 +1116,7 @@ int bias_grad(Trainer* T, const float* dy, int ld, int C, int R, float* dst) {
     const int nb = nblk_rows(R);
     dim3 g(nb, (C + 63) / 64);
     tr::launch_colsum<0>(g, T->st, dy, ld, C, R, nullptr, nullptr, nullptr, nullptr, T->cpart,
-                         {tr::FIN_SUM, dst, nullptr, nullptr, nullptr, T->cctr});
+                         {tr::FIN_SUM, dst, nullptr, nullptr, nullptr});
     return hipGetLastError() == hipSuccess ? 0 : fail("bias grad failed");
 }
 
@@ -1467,7 +1398,6 @@ int az_trainer_create(int blocks, int filters, const float* weights, size_t n, i
     T->wpart = A(wp);
     T->wpart_cap = wp;
     T->cpart = A((R / tr::CS_ROWS + 2) * 2 * (size_t)std::max(F, 65));
-    T->cctr = reinterpret_cast<int*>(A(64));
     // dW scratch: input conv [9][64][F], residual conv [9][F][F], heads [F][64] + its [40][F]
     // transpose, policy_conv_2 [32][64], value_linear_2 partial sums (65)
     T->dwtmp_cap = std::max({(size_t)9 * 64 * F, (size_t)9 * F * F, (size_t)F * 64 + 40 * (size_t)F, (size_t)32 * 64,
@@ -1499,8 +1429,7 @@ int az_trainer_create(int blocks, int filters, const float* weights, size_t n, i
         return fail("az_trainer_create: upload failed");
     }
     // the Winograd weight buffers' prefetch pad stays zero (the per-step transforms write the rest)
-    if ((T->ubase && hipMemset(T->ubase, 0, 2 * (size_t)(nconv - 1) * T->ubytes) != hipSuccess) ||
-        hipMemset(T->cctr, 0, 64 * sizeof(int)) != hipSuccess) {
+    if (T->ubase && hipMemset(T->ubase, 0, 2 * (size_t)(nconv - 1) * T->ubytes) != hipSuccess) {
         delete T;
         return fail("az_trainer_create: upload failed");
     }
