@@ -509,6 +509,27 @@ __global__ void finalize_bnback_kernel(const float* __restrict__ part, int nblk,
         dgamma[c] = g;
     }
 }
+// BN forward statistics from per-board partials (BoardStats, STATS 1): mean = sum / R, and the
+// squared deviations combined as sum_b [M2_b + 64 (mean_b - mean)^2] (Chan, Golub & LeVeque's
+// pairwise update, every board 64 rows); then as finalize_var_kernel.  Fixed order per channel.
+__global__ void bn_board_var_kernel(const float* __restrict__ part, int nb, int C, int R, float* __restrict__ mean,
+                                    float* __restrict__ stdv, float* __restrict__ rmean, float* __restrict__ rvar) {
+    FIN_CHANNEL();
+    const float mu = part_sum(part, nb, C, c, 0, lane) / (float)R;
+    float m2 = 0.0f;
+    for (int b = lane; b < nb; b += 64) {
+        const float d = part[((size_t)b * 2) * C + c] / 64.0f - mu;
+        m2 += part[((size_t)b * 2 + 1) * C + c] + 64.0f * (d * d);
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) m2 += __shfl_xor(m2, m, 64);
+    if (lane != 0) return;
+    const float var = m2 / (float)R;
+    mean[c] = mu;
+    stdv[c] = sqrtf(var + 1e-5f);
+    rmean[c] = rmean[c] * 0.9f + mu * 0.1f;
+    rvar[c] = rvar[c] * 0.9f + var * 0.1f;
+}
 #undef FIN_CHANNEL
 
 // column sums (16-byte loads when the channel layout allows it, else the scalar kernel), then the
@@ -593,8 +614,9 @@ __global__ void __launch_bounds__(256) bn_back4_kernel(const float* __restrict__
                                                        const float* __restrict__ mean, const float* __restrict__ stdv,
                                                        const float* __restrict__ gamma, const float* __restrict__ dgamma,
                                                        const float* __restrict__ dbeta, float* __restrict__ dy,
-                                                       float* __restrict__ dres) {
+                                                       float* __restrict__ dres, float* __restrict__ bsum) {
     const int cq = C / 4, c = 4 * (threadIdx.x % cq), rs = 256 / cq;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);   // bsum: this thread's rows of dy, in order
     const float invR = 1.0f / (float)R;
     const float4 mu = *reinterpret_cast<const float4*>(mean + c), sd = *reinterpret_cast<const float4*>(stdv + c);
     const float4 ga = *reinterpret_cast<const float4*>(gamma + c), dg = *reinterpret_cast<const float4*>(dgamma + c);
@@ -605,12 +627,28 @@ __global__ void __launch_bounds__(256) bn_back4_kernel(const float* __restrict__
         const float4 y = *reinterpret_cast<const float4*>(Y + o);
         const float4 dz = make_float4(ov.x > 0.0f ? d.x : 0.0f, ov.y > 0.0f ? d.y : 0.0f, ov.z > 0.0f ? d.z : 0.0f,
                                       ov.w > 0.0f ? d.w : 0.0f);
-        *reinterpret_cast<float4*>(dy + o) =
-            make_float4((ga.x / sd.x) * (dz.x - db.x * invR - ((y.x - mu.x) / sd.x) * dg.x * invR),
-                        (ga.y / sd.y) * (dz.y - db.y * invR - ((y.y - mu.y) / sd.y) * dg.y * invR),
-                        (ga.z / sd.z) * (dz.z - db.z * invR - ((y.z - mu.z) / sd.z) * dg.z * invR),
-                        (ga.w / sd.w) * (dz.w - db.w * invR - ((y.w - mu.w) / sd.w) * dg.w * invR));
+        const float4 d4 = make_float4((ga.x / sd.x) * (dz.x - db.x * invR - ((y.x - mu.x) / sd.x) * dg.x * invR),
+                                      (ga.y / sd.y) * (dz.y - db.y * invR - ((y.y - mu.y) / sd.y) * dg.y * invR),
+                                      (ga.z / sd.z) * (dz.z - db.z * invR - ((y.z - mu.z) / sd.z) * dg.z * invR),
+                                      (ga.w / sd.w) * (dz.w - db.w * invR - ((y.w - mu.w) / sd.w) * dg.w * invR));
+        *reinterpret_cast<float4*>(dy + o) = d4;
         if (dres) *reinterpret_cast<float4*>(dres + o) = dz;
+        acc.x += d4.x; acc.y += d4.y; acc.z += d4.z; acc.w += d4.w;
+    }
+    // the conv bias gradient (sum of dy over rows) as per-workgroup partials in the column-sum
+    // layout part[block][2][C] (finalize_sum_kernel), instead of another pass over dy
+    if (bsum) {
+        __shared__ float4 red[256];
+        red[threadIdx.x] = acc;
+        __syncthreads();
+        if ((int)threadIdx.x < cq) {
+            float4 a = red[threadIdx.x];
+            for (int k = 1; k < rs; k++) {
+                const float4 b = red[k * cq + threadIdx.x];
+                a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+            }
+            *reinterpret_cast<float4*>(bsum + (size_t)blockIdx.x * 2 * C + c) = a;
+        }
     }
 }
 
@@ -721,10 +759,32 @@ loss_kernel(const float* __restrict__ logits, const float* __restrict__ tpol, co
 // per 512-thread workgroup: the board's 64 rows of X into LDS, wino_core, Y (+ addend) back to
 // HBM with no ReLU (BatchNorm runs in training mode after it).  The data grad is the same conv of
 // dY with the flipped, transposed kernel (U built by wino_weights_kernel with flip = 1).
-template <bool ADD>
+// STATS: per-board BatchNorm statistics of the output from the epilogue, into part[board][2][F]
+// (the layout of the column-sum partials, one "row block" per board):
+//   1 (forward, the output is the BN input): sum and sum of squared deviations from the board's
+//     own mean -- combined over boards by bn_board_var_kernel (Chan et al.'s pairwise update);
+//   2 (data grad, the output is the BN backward's dout): sum dz and sum dz * yhat with
+//     dz = dout * (O > 0), yhat = (Ybn - mean) / std -- summed over boards by finalize_bnback_kernel.
+// Either replaces two passes over the 32 MB output (colsum4 + finalize twice, or colsum4<2>).
+struct BoardStats {
+    float* part;
+    const float* O;      // STATS 2: the BN's ReLU output
+    const float* Ybn;    // STATS 2: the BN's input
+    const float* mean;   // STATS 2
+    const float* stdv;   // STATS 2
+};
+__device__ __forceinline__ f32x4 sum16(f32x4 v) {   // over the 16 lanes of a row (fixed butterfly)
+#pragma unroll
+    for (int m = 1; m < 16; m <<= 1)
+#pragma unroll
+        for (int r = 0; r < 4; r++) v[r] += __shfl_xor(v[r], m, 64);
+    return v;
+}
+template <bool ADD, int STATS>
 __global__ void __launch_bounds__(512)
 conv_wino_train_kernel(const float* __restrict__ X, const uint4* __restrict__ U, unsigned ubytes,
-                       const float* __restrict__ bias, const float* __restrict__ addend, float* __restrict__ Y) {
+                       const float* __restrict__ bias, const float* __restrict__ addend, float* __restrict__ Y,
+                       BoardStats bs) {
     constexpr int F = 256, NN = WinoCfg<F>::NN, XSn = WinoCfg<F>::XS, PF = WinoCfg<F>::PF, RS = F / 4 + 2;
     constexpr int XSZ = 64 * RS, VSZ = 2 * WinoCfg<F>::CH * 1024 / 16, PAD = WINO_PAD_SQ * RS;
     __shared__ __attribute__((aligned(16))) uint4 lds[PAD + XSZ + PAD + VSZ];
@@ -754,15 +814,57 @@ conv_wino_train_kernel(const float* __restrict__ X, const uint4* __restrict__ U,
     wino_core<F>(reinterpret_cast<char*>(act), (XSZ + PAD) * 16, rW, rN, bias, wr, w, lane, y);
     const int l16 = lane & 15, h = lane >> 4, ty = l16 >> 2, tx = l16 & 3;
     const int co0 = w * 16 * NN + h * 4;
+    f32x4 s0[NN], s1[NN];
 #pragma unroll
-    for (int n = 0; n < NN; n++)
+    for (int n = 0; n < NN; n++) {
+        s0[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+        s1[n] = s0[n];
+        f32x4 mu = s0[n], sd = s0[n];
+        if constexpr (STATS == 2) {
+            mu = *reinterpret_cast<const f32x4*>(bs.mean + co0 + n * 16);
+            sd = *reinterpret_cast<const f32x4*>(bs.stdv + co0 + n * 16);
+        }
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const size_t o = (row0 + (2 * ty + (q >> 1)) * 8 + 2 * tx + (q & 1)) * F + co0 + n * 16;
             f32x4 v = y[n][q];
             if constexpr (ADD) v += *reinterpret_cast<const f32x4*>(addend + o);
             *reinterpret_cast<f32x4*>(Y + o) = v;
+            if constexpr (STATS == 1) {
+                y[n][q] = v;
+                s0[n] += v;
+            } else if constexpr (STATS == 2) {
+                const f32x4 ov = *reinterpret_cast<const f32x4*>(bs.O + o);
+                const f32x4 yb = *reinterpret_cast<const f32x4*>(bs.Ybn + o);
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const float dz = ov[r] > 0.0f ? v[r] : 0.0f;
+                    s0[n][r] += dz;
+                    s1[n][r] += dz * ((yb[r] - mu[r]) / sd[r]);
+                }
+            }
         }
+    }
+    if constexpr (STATS != 0) {
+#pragma unroll
+        for (int n = 0; n < NN; n++) {
+            s0[n] = sum16(s0[n]);
+            if constexpr (STATS == 1) {
+                const f32x4 mb = s0[n] / 64.0f;   // the board's mean (64 squares)
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const f32x4 d = y[n][q] - mb;
+                    s1[n] += d * d;
+                }
+            }
+            s1[n] = sum16(s1[n]);
+            if (l16 == 0) {
+                float* pb = bs.part + (size_t)vgpr_index(blockIdx.x) * 2 * F + co0 + n * 16;
+                *reinterpret_cast<f32x4*>(pb) = s0[n];
+                *reinterpret_cast<f32x4*>(pb + F) = s1[n];
+            }
+        }
+    }
 }
 
 // Winograd weights U = G g G^T (f64, rounded once to f32: the same arithmetic as net.hip's
@@ -959,6 +1061,9 @@ struct Trainer {
     float *bmean = nullptr, *bstd = nullptr, *dgb = nullptr;
     // reduction scratch
     float *wpart = nullptr, *cpart = nullptr, *dwtmp = nullptr;
+    float* bpart = nullptr;                  // per-board BN partials [Bmax][2][F] (tr::BoardStats)
+    float* bsum = nullptr;                   // conv bias-grad partials of bn_back4_kernel [grid][2][C]
+    size_t bsum_cap = 0;
     size_t wpart_cap = 0, dwtmp_cap = 0;
     int slot = 0;                            // per-BN statistics stride (>= every BN's channels)
     float *tpol = nullptr, *tval = nullptr, *planes = nullptr, *loss = nullptr, *vpart = nullptr;
@@ -1004,14 +1109,25 @@ int launch_conv(Trainer* T, int taps, const float* X, int ldx, int K, const floa
     return hipGetLastError() == hipSuccess ? 0 : fail("conv launch failed");
 }
 
-// Y = conv3x3(X, U) (+ bias) (+ addend) over B whole boards, Winograd (F = 256 residual convs)
-int launch_wino(Trainer* T, const float* X, const float* U, const float* bias, const float* addend, float* Y, int B) {
-    if (addend)
-        tr::conv_wino_train_kernel<true><<<B, 512, 0, T->st>>>(X, reinterpret_cast<const uint4*>(U), (unsigned)T->ubytes,
-                                                                bias, addend, Y);
+// Y = conv3x3(X, U) (+ bias) (+ addend) over B whole boards, Winograd (F = 256 residual convs);
+// stats 1 / 2: per-board BN partials into bs.part (tr::BoardStats)
+int launch_wino(Trainer* T, const float* X, const float* U, const float* bias, const float* addend, float* Y, int B,
+                int stats = 0, tr::BoardStats bs = {}) {
+    const uint4* U4 = reinterpret_cast<const uint4*>(U);
+    const unsigned ub = (unsigned)T->ubytes;
+    if (stats && !bs.part) return fail("Winograd conv: statistics without a buffer");
+    if (addend && stats == 2)
+        tr::conv_wino_train_kernel<true, 2><<<B, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs);
+    else if (addend && stats == 0)
+        tr::conv_wino_train_kernel<true, 0><<<B, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs);
+    else if (!addend && stats == 1)
+        tr::conv_wino_train_kernel<false, 1><<<B, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs);
+    else if (!addend && stats == 2)
+        tr::conv_wino_train_kernel<false, 2><<<B, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs);
+    else if (!addend && stats == 0)
+        tr::conv_wino_train_kernel<false, 0><<<B, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs);
     else
-        tr::conv_wino_train_kernel<false><<<B, 512, 0, T->st>>>(X, reinterpret_cast<const uint4*>(U), (unsigned)T->ubytes,
-                                                                 bias, nullptr, Y);
+        return fail("Winograd conv: unsupported statistics mode");
     return hipGetLastError() == hipSuccess ? 0 : fail("Winograd conv launch failed");
 }
 
@@ -1074,17 +1190,26 @@ unsigned bn_grid(int C, int R) {
 }
 
 // BatchNorm (training) + ReLU (+ residual): Y -> out; saves mean/std in slot `bi`
-int bn_forward(Trainer* T, int bi, const float* Y, int ld, int C, int R, size_t bn_off, const float* res, float* out) {
+// bpart: per-board partials from the producing conv's epilogue (tr::BoardStats, STATS 1) instead
+// of the two column-sum passes
+int bn_forward(Trainer* T, int bi, const float* Y, int ld, int C, int R, size_t bn_off, const float* res, float* out,
+               const float* bpart = nullptr) {
     float* P = T->p + bn_off;   // {gamma, beta, running_mean, running_var}
     if (C > T->slot) return fail("bn: too many channels");
     float* mean = T->bmean + (size_t)bi * T->slot;
     float* sd = T->bstd + (size_t)bi * T->slot;
-    const int nb = nblk_rows(R);
-    dim3 g(nb, (C + 63) / 64);
-    tr::launch_colsum<0>(g, T->st, Y, ld, C, R, nullptr, nullptr, nullptr, nullptr, T->cpart,
-                         {tr::FIN_MEAN, mean, nullptr, nullptr, nullptr});
-    tr::launch_colsum<1>(g, T->st, Y, ld, C, R, mean, nullptr, nullptr, nullptr, T->cpart,
-                         {tr::FIN_VAR, sd, P + 2 * C, P + 3 * C, mean});
+    if (bpart) {
+        if (R % 64 || ld != C) return fail("bn: board statistics need whole boards");
+        tr::bn_board_var_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(bpart, R / 64, C, R, mean, sd, P + 2 * C,
+                                                                        P + 3 * C);
+    } else {
+        const int nb = nblk_rows(R);
+        dim3 g(nb, (C + 63) / 64);
+        tr::launch_colsum<0>(g, T->st, Y, ld, C, R, nullptr, nullptr, nullptr, nullptr, T->cpart,
+                             {tr::FIN_MEAN, mean, nullptr, nullptr, nullptr});
+        tr::launch_colsum<1>(g, T->st, Y, ld, C, R, mean, nullptr, nullptr, nullptr, T->cpart,
+                             {tr::FIN_VAR, sd, P + 2 * C, P + 3 * C, mean});
+    }
     if (bn_vec(C, ld, {Y, res, out, P, mean, sd}))
         tr::bn_apply4_kernel<<<bn_grid(C, R), 256, 0, T->st>>>(Y, ld, C, R, mean, sd, P, P + C, res, out);
     else
@@ -1093,22 +1218,35 @@ int bn_forward(Trainer* T, int bi, const float* Y, int ld, int C, int R, size_t 
 }
 
 // BN backward: dout (grad of the ReLU output O), pre-BN Y -> dy; dgamma/dbeta into the grad buffer
+// bpart: per-board dz / dz*yhat sums from the conv that produced dout (tr::BoardStats, STATS 2)
+// bias: the producing conv's bias gradient (sum of dy over rows), fused into the BN backward
+int bias_grad(Trainer* T, const float* dy, int ld, int C, int R, float* dst);
 int bn_backward(Trainer* T, int bi, const float* dout, const float* O, const float* Y, int ld, int C, int R,
-                size_t bn_off, float* dy, float* dres) {
+                size_t bn_off, float* dy, float* dres, const float* bpart = nullptr, float* bias = nullptr) {
     const float* mean = T->bmean + (size_t)bi * T->slot;
     const float* sd = T->bstd + (size_t)bi * T->slot;
-    const int nb = nblk_rows(R);
-    dim3 g(nb, (C + 63) / 64);
     float* dgam = T->g + bn_off;
     float* dbet = T->g + bn_off + C;
-    tr::launch_colsum<2>(g, T->st, dout, ld, C, R, mean, sd, O, Y, T->cpart,
-                         {tr::FIN_BNBACK, dgam, dbet, nullptr, nullptr});
-    if (bn_vec(C, ld, {dout, O, Y, dy, dres, T->p + bn_off, dgam, mean, sd}))
-        tr::bn_back4_kernel<<<bn_grid(C, R), 256, 0, T->st>>>(dout, O, Y, ld, C, R, mean, sd, T->p + bn_off, dgam, dbet,
-                                                              dy, dres);
-    else
+    if (bpart) {
+        if (R % 64 || ld != C) return fail("bn: board statistics need whole boards");
+        tr::finalize_bnback_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(bpart, R / 64, C, dgam, dbet);
+    } else {
+        const int nb = nblk_rows(R);
+        dim3 g(nb, (C + 63) / 64);
+        tr::launch_colsum<2>(g, T->st, dout, ld, C, R, mean, sd, O, Y, T->cpart,
+                             {tr::FIN_BNBACK, dgam, dbet, nullptr, nullptr});
+    }
+    if (bn_vec(C, ld, {dout, O, Y, dy, dres, T->p + bn_off, dgam, mean, sd})) {
+        const unsigned g = bn_grid(C, R);
+        if (bias && (size_t)g * 2 * C > T->bsum_cap) return fail("bn: bias partial buffer too small");
+        tr::bn_back4_kernel<<<g, 256, 0, T->st>>>(dout, O, Y, ld, C, R, mean, sd, T->p + bn_off, dgam, dbet, dy, dres,
+                                                  bias ? T->bsum : nullptr);
+        if (bias) tr::finalize_sum_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(T->bsum, (int)g, C, bias);
+    } else {
         tr::bn_back_kernel<<<grid_for((size_t)R * C), 256, 0, T->st>>>(dout, O, Y, ld, C, R, mean, sd, T->p + bn_off,
                                                                        dgam, dbet, dy, dres);
+        if (bias && bias_grad(T, dy, ld, C, R, bias) != 0) return -1;
+    }
     return hipGetLastError() == hipSuccess ? 0 : fail("bn backward failed");
 }
 
@@ -1169,12 +1307,14 @@ int trainer_grads(Trainer* T, const float* planes, const float* tpol, const floa
     for (int b = 0; b < T->blocks; b++) {
         const auto& c1 = L.tower[1 + 2 * b];
         const auto& c2 = L.tower[2 + 2 * b];
-        if (T->wino) TRY(launch_wino(T, T->xs[b], T->uf[1 + 2 * b], T->p + c1.b, nullptr, T->y1[b], B));
+        // Winograd convs hand their BN the per-board statistics (bpart) from their epilogue
+        const float* bp = T->wino ? T->bpart : nullptr;
+        if (T->wino) TRY(launch_wino(T, T->xs[b], T->uf[1 + 2 * b], T->p + c1.b, nullptr, T->y1[b], B, 1, {T->bpart}));
         else TRY(launch_conv(T, 9, T->xs[b], F, F, T->wf[1 + 2 * b], F, T->p + c1.b, nullptr, T->y1[b], F, R));
-        TRY(bn_forward(T, 1 + 2 * b, T->y1[b], F, F, R, c1.bn, nullptr, T->hh[b]));
-        if (T->wino) TRY(launch_wino(T, T->hh[b], T->uf[2 + 2 * b], T->p + c2.b, nullptr, T->y2[b], B));
+        TRY(bn_forward(T, 1 + 2 * b, T->y1[b], F, F, R, c1.bn, nullptr, T->hh[b], bp));
+        if (T->wino) TRY(launch_wino(T, T->hh[b], T->uf[2 + 2 * b], T->p + c2.b, nullptr, T->y2[b], B, 1, {T->bpart}));
         else TRY(launch_conv(T, 9, T->hh[b], F, F, T->wf[2 + 2 * b], F, T->p + c2.b, nullptr, T->y2[b], F, R));
-        TRY(bn_forward(T, 2 + 2 * b, T->y2[b], F, F, R, c2.bn, T->xs[b], T->xs[b + 1]));
+        TRY(bn_forward(T, 2 + 2 * b, T->y2[b], F, F, R, c2.bn, T->xs[b], T->xs[b + 1], bp));
     }
     const float* body = T->xs[T->blocks];
     const int nbn = 1 + 2 * T->blocks;
@@ -1222,32 +1362,43 @@ int trainer_grads(Trainer* T, const float* planes, const float* tpol, const floa
     TRY(bias_grad(T, T->dy40 + 32, 64, 8, R, T->g + L.vb));
     TRY(launch_conv(T, 1, T->dy40, 64, 64, T->w40d, F, nullptr, nullptr, T->dx, F, R));
     // residual tower, last block first
+    // dout of every BN but the last block's second comes from a Winograd data-grad conv, whose
+    // epilogue leaves the BN backward's per-board sums in bpart (dx_stats: dx came with them)
+    bool dx_stats = false;
     for (int b = T->blocks - 1; b >= 0; b--) {
         const auto& c1 = L.tower[1 + 2 * b];
         const auto& c2 = L.tower[2 + 2 * b];
-        TRY(bn_backward(T, 2 + 2 * b, T->dx, T->xs[b + 1], T->y2[b], F, F, R, c2.bn, T->dy, T->dres));
-        TRY(bias_grad(T, T->dy, F, F, R, T->g + c2.b));
+        auto bstat = [&](int bi, const float* O, const float* Ybn) {
+            return tr::BoardStats{T->bpart, O, Ybn, T->bmean + (size_t)bi * T->slot, T->bstd + (size_t)bi * T->slot};
+        };
+        TRY(bn_backward(T, 2 + 2 * b, T->dx, T->xs[b + 1], T->y2[b], F, F, R, c2.bn, T->dy, T->dres,
+                        dx_stats ? T->bpart : nullptr, T->g + c2.b));
         if (T->wino) TRY(launch_wino_wgrad(T, T->hh[b], T->dy, B, T->g + c2.w));
         else {
             TRY(launch_wgrad(T, 9, T->hh[b], F, F, T->dy, F, F, R, T->dwtmp, T->dwtmp_cap));
             tr::unpack3x3_kernel<<<grid_for((size_t)9 * F * F), 256, 0, st>>>(T->dwtmp, F, F, F, T->g + c2.w);
         }
-        if (T->wino) TRY(launch_wino(T, T->dy, T->ud[2 + 2 * b], nullptr, nullptr, T->dh, B));
+        if (T->wino)
+            TRY(launch_wino(T, T->dy, T->ud[2 + 2 * b], nullptr, nullptr, T->dh, B, 2, bstat(1 + 2 * b, T->hh[b], T->y1[b])));
         else TRY(launch_conv(T, 9, T->dy, F, F, T->wd[2 + 2 * b], F, nullptr, nullptr, T->dh, F, R));
-        TRY(bn_backward(T, 1 + 2 * b, T->dh, T->hh[b], T->y1[b], F, F, R, c1.bn, T->dy, nullptr));
-        TRY(bias_grad(T, T->dy, F, F, R, T->g + c1.b));
+        TRY(bn_backward(T, 1 + 2 * b, T->dh, T->hh[b], T->y1[b], F, F, R, c1.bn, T->dy, nullptr,
+                        T->wino ? T->bpart : nullptr, T->g + c1.b));
         if (T->wino) TRY(launch_wino_wgrad(T, T->xs[b], T->dy, B, T->g + c1.w));
         else {
             TRY(launch_wgrad(T, 9, T->xs[b], F, F, T->dy, F, F, R, T->dwtmp, T->dwtmp_cap));
             tr::unpack3x3_kernel<<<grid_for((size_t)9 * F * F), 256, 0, st>>>(T->dwtmp, F, F, F, T->g + c1.w);
         }
-        if (T->wino) TRY(launch_wino(T, T->dy, T->ud[1 + 2 * b], nullptr, T->dres, T->dxn, B));
+        // dx is the gradient of block b's input: the output of BN 2b (BN 0 = the input conv's)
+        if (T->wino)
+            TRY(launch_wino(T, T->dy, T->ud[1 + 2 * b], nullptr, T->dres, T->dxn, B, 2, bstat(2 * b, T->xs[b],
+                                                                                            b > 0 ? T->y2[b - 1] : T->y0)));
         else TRY(launch_conv(T, 9, T->dy, F, F, T->wd[1 + 2 * b], F, nullptr, T->dres, T->dxn, F, R));
+        dx_stats = T->wino;
         std::swap(T->dx, T->dxn);
     }
     // input conv (no data grad)
-    TRY(bn_backward(T, 0, T->dx, T->xs[0], T->y0, F, F, R, L.tower[0].bn, T->dy, nullptr));
-    TRY(bias_grad(T, T->dy, F, F, R, T->g + L.tower[0].b));
+    TRY(bn_backward(T, 0, T->dx, T->xs[0], T->y0, F, F, R, L.tower[0].bn, T->dy, nullptr, dx_stats ? T->bpart : nullptr,
+                    T->g + L.tower[0].b));
     TRY(launch_wgrad(T, 9, T->x0, 64, 64, T->dy, F, F, R, T->dwtmp, T->dwtmp_cap));
     tr::unpack3x3_kernel<<<grid_for((size_t)9 * 19 * F), 256, 0, st>>>(T->dwtmp, F, 19, 64, T->g + L.tower[0].w);
     AZ_HIP(hipMemcpyAsync(T->hloss, T->loss, (size_t)B * 2 * sizeof(float), hipMemcpyDeviceToHost, st));
@@ -1398,6 +1549,9 @@ int az_trainer_create(int blocks, int filters, const float* weights, size_t n, i
     T->wpart = A(wp);
     T->wpart_cap = wp;
     T->cpart = A((R / tr::CS_ROWS + 2) * 2 * (size_t)std::max(F, 65));
+    T->bpart = A((size_t)max_batch * 2 * F);
+    T->bsum_cap = (size_t)256 * 4 * 2 * std::max(F, 64);   // bn_grid's workgroup cap x [2][C]
+    T->bsum = A(T->bsum_cap);
     // dW scratch: input conv [9][64][F], residual conv [9][F][F], heads [F][64] + its [40][F]
     // transpose, policy_conv_2 [32][64], value_linear_2 partial sums (65)
     T->dwtmp_cap = std::max({(size_t)9 * 64 * F, (size_t)9 * F * F, (size_t)F * 64 + 40 * (size_t)F, (size_t)32 * 64,
