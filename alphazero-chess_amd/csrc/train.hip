@@ -247,51 +247,63 @@ constexpr int WG_S = 256 + 16;
 // the four F(2x2,3x3) combinations: (a, b) = (e0, e2) / (e1, e2) / (e1, e2) / (e1, e3) of a patch
 // row or column -> a - b, a + b, b - a, a - b (B^T rows)
 __device__ __forceinline__ f32x4 wino_comb(int k, f32x4 a, f32x4 b) { return k == 1 ? a + b : k == 2 ? b - a : a - b; }
-__global__ void __launch_bounds__(512)
+// NWG waves: 8 (wave w owns co [32 w, 32 w + 32), two tiles staged per thread) or 16 (co [16 w,
+// 16 w + 16), one tile per thread, 4 waves per SIMD at <= 128 VGPRs); every dU element takes the
+// same MFMAs in the same order either way (bit-identical).
+template <int NWG>
+__global__ void __launch_bounds__(NWG * 64)
 wino_wgrad_gemm_kernel(const float* __restrict__ X, const float* __restrict__ DY, int K, int rows_per_split,
                        float* __restrict__ partial) {
-    constexpr int F = 256;
+    constexpr int F = 256, CO = F / NWG, NN = CO / 16, TPT = 16 / NWG;
+    static_assert(NWG == 8 || NWG == 16, "8 or 16 waves");
     __shared__ __attribute__((aligned(16))) float xs[16 * WG_S];
     __shared__ __attribute__((aligned(16))) float ds[16 * WG_S];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int split = blockIdx.x, xi = blockIdx.y, r = xi >> 2, q = xi & 3;
     const int i1 = r == 0 ? 0 : 1, i2 = r == 3 ? 3 : 2, j1 = q == 0 ? 0 : 1, j2 = q == 3 ? 3 : 2;
     const int rbeg = split * rows_per_split, rend = min(K, rbeg + rows_per_split);
-    f32x4 acc[16][2];
+    f32x4 acc[16][NN];
 #pragma unroll
     for (int b = 0; b < 16; b++)
 #pragma unroll
-        for (int n = 0; n < 2; n++) acc[b][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // staging: thread = (channel quad c4, tiles 2 tp and 2 tp + 1)
-    const int c4 = (tid & 63) * 4, tp = tid >> 6;
-    f32x4 xd[2][2][2], yv[2][2][2];   // [tile][patch row i1 / i2][patch column j1 / j2], [tile][a][b]
+        for (int n = 0; n < NN; n++) acc[b][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // staging: thread = (channel quad c4, tiles TPT tp .. TPT tp + TPT - 1).  The squares come in
+    // through buffer loads: the lane's channel offset is the only VGPR address, the (wave-uniform)
+    // square offset rides in the SGPR offset, and an off-board square is an offset past the buffer's
+    // end, which the hardware reads as 0 (no branch, no 64-bit address per load)
+    const int c4 = (tid & 63) * 4, tp = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int xbytes = (K >> 4) * 64 * F * 4;   // K (board, tile) rows = K / 16 boards
+    const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, xbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rD = __builtin_amdgcn_make_buffer_rsrc((void*)DY, (short)0, xbytes, 0x00020000);
+    constexpr int OFF_BOARD = 0x40000000;       // past any buffer this kernel is given (< 1 GiB, host-checked)
+    f32x4 xd[TPT][2][2], yv[TPT][2][2];   // [tile][patch row i1 / i2][patch column j1 / j2], [tile][a][b]
     auto fetch = [&](int rc) {
-        const size_t b64 = (size_t)(rc >> 4) * 64;
+        const int bb0 = (rc >> 4) * 64 * F * 4;
 #pragma unroll
-        for (int u = 0; u < 2; u++) {
-            const int t = 2 * tp + u, ty = t >> 2, tx = t & 3;
+        for (int u = 0; u < TPT; u++) {
+            const int t = TPT * tp + u, ty = t >> 2, tx = t & 3;
 #pragma unroll
             for (int ii = 0; ii < 2; ii++)
 #pragma unroll
                 for (int jj = 0; jj < 2; jj++) {
                     const int row = 2 * ty - 1 + (ii ? i2 : i1), col = 2 * tx - 1 + (jj ? j2 : j1);
-                    xd[u][ii][jj] = ((unsigned)row < 8u && (unsigned)col < 8u)
-                                        ? *reinterpret_cast<const f32x4*>(X + (b64 + row * 8 + col) * F + c4)
-                                        : f32x4{0.f, 0.f, 0.f, 0.f};
+                    const int so = ((unsigned)row < 8u && (unsigned)col < 8u) ? bb0 + (row * 8 + col) * F * 4 : OFF_BOARD;
+                    xd[u][ii][jj] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rX, c4 * 4, so, 0));
                 }
 #pragma unroll
             for (int a = 0; a < 2; a++)
 #pragma unroll
                 for (int bb = 0; bb < 2; bb++)
-                    yv[u][a][bb] = *reinterpret_cast<const f32x4*>(DY + (b64 + (2 * ty + a) * 8 + 2 * tx + bb) * F + c4);
+                    yv[u][a][bb] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                 rD, c4 * 4, bb0 + ((2 * ty + a) * 8 + 2 * tx + bb) * F * 4, 0));
         }
     };
     if (rbeg < rend) fetch(rbeg);
     for (int rc = rbeg; rc < rend; rc += 16) {
         __syncthreads();
 #pragma unroll
-        for (int u = 0; u < 2; u++) {
-            const int t = 2 * tp + u;
+        for (int u = 0; u < TPT; u++) {
+            const int t = TPT * tp + u;
             // V: rows first (tt over the two columns), then the column combination
             const f32x4 tt1 = wino_comb(r, xd[u][0][0], xd[u][1][0]), tt2 = wino_comb(r, xd[u][0][1], xd[u][1][1]);
             const f32x4 v = wino_comb(q, tt1, tt2);
@@ -314,16 +326,17 @@ wino_wgrad_gemm_kernel(const float* __restrict__ X, const float* __restrict__ DY
 #pragma unroll
         for (int qq = 0; qq < 4; qq++) {
             const int rq = qq * 4 + (lane >> 4);
-            const float b0 = ds[rq * WG_S + 32 * w + (lane & 15)];
-            const float b1 = ds[rq * WG_S + 32 * w + 16 + (lane & 15)];
+            float bv[NN];
+#pragma unroll
+            for (int n = 0; n < NN; n++) bv[n] = ds[rq * WG_S + CO * w + 16 * n + (lane & 15)];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const f32x4 a = *reinterpret_cast<const f32x4*>(xs + rq * WG_S + 64 * j + 4 * (lane & 15));
 #pragma unroll
-                for (int c = 0; c < 4; c++) {
-                    acc[4 * j + c][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c], b0, acc[4 * j + c][0], 0, 0, 0);
-                    acc[4 * j + c][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c], b1, acc[4 * j + c][1], 0, 0, 0);
-                }
+                for (int c = 0; c < 4; c++)
+#pragma unroll
+                    for (int n = 0; n < NN; n++)
+                        acc[4 * j + c][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c], bv[n], acc[4 * j + c][n], 0, 0, 0);
             }
         }
     }
@@ -333,10 +346,10 @@ wino_wgrad_gemm_kernel(const float* __restrict__ X, const float* __restrict__ DY
 #pragma unroll
         for (int c = 0; c < 4; c++)
 #pragma unroll
-            for (int n = 0; n < 2; n++)
+            for (int n = 0; n < NN; n++)
 #pragma unroll
                 for (int g = 0; g < 4; g++) {
-                    const int ci = 64 * j + 4 * (4 * (lane >> 4) + g) + c, co = 32 * w + 16 * n + (lane & 15);
+                    const int ci = 64 * j + 4 * (4 * (lane >> 4) + g) + c, co = CO * w + 16 * n + (lane & 15);
                     out[(size_t)ci * F + co] = acc[4 * j + c][n][g];
                 }
 }
@@ -1062,6 +1075,7 @@ struct Trainer {
     // reduction scratch
     float *wpart = nullptr, *cpart = nullptr, *dwtmp = nullptr;
     float* bpart = nullptr;                  // per-board BN partials [Bmax][2][F] (tr::BoardStats)
+    int wgrad_waves = 8;                     // wino_wgrad_gemm_kernel<8 | 16> (AZ_WGRAD_WAVES)
     float* bsum = nullptr;                   // conv bias-grad partials of bn_back4_kernel [grid][2][C]
     size_t bsum_cap = 0;
     size_t wpart_cap = 0, dwtmp_cap = 0;
@@ -1166,8 +1180,12 @@ int launch_wino_wgrad(Trainer* T, const float* X, const float* DY, int B, float*
     if (B > T->Bmax) return fail("Winograd wgrad: batch too large");
     const int splits = (int)wino_gemm_splits(B);
     if (splits * 16 * (size_t)F * F > T->wpart_cap) return fail("Winograd wgrad: partial buffer too small");
+    if ((size_t)B * 64 * F * 4 >= (size_t)0x40000000) return fail("Winograd wgrad: batch too large for 32-bit offsets");
     hipStream_t st = T->st;
-    tr::wino_wgrad_gemm_kernel<<<dim3(splits, 16), 512, 0, st>>>(X, DY, K, WINO_GEMM_ROWS, T->wpart);
+    if (T->wgrad_waves == 16)
+        tr::wino_wgrad_gemm_kernel<16><<<dim3(splits, 16), 1024, 0, st>>>(X, DY, K, WINO_GEMM_ROWS, T->wpart);
+    else
+        tr::wino_wgrad_gemm_kernel<8><<<dim3(splits, 16), 512, 0, st>>>(X, DY, K, WINO_GEMM_ROWS, T->wpart);
     if ((size_t)F * F % 64) return fail("Winograd wgrad: F * F must be a multiple of 64");
     tr::wino_wgrad_reduce_out_kernel<<<(unsigned)((size_t)F * F / 64), 1024, 0, st>>>(T->wpart, splits, F, g);
     return hipGetLastError() == hipSuccess ? 0 : fail("Winograd wgrad launch failed");
@@ -1513,6 +1531,7 @@ int az_trainer_create(int blocks, int filters, const float* weights, size_t n, i
     const int nconv = 1 + 2 * blocks;
     T->wino = F == 256;
     if (const char* e = getenv("AZ_TRAIN_WINOGRAD")) T->wino = T->wino && atoi(e) != 0;
+    if (const char* e = getenv("AZ_WGRAD_WAVES")) T->wgrad_waves = atoi(e) == 16 ? 16 : 8;
     // Winograd U per residual conv: 16 points x F x F + 8 zero ring steps of prefetch pad
     const size_t ufl = (size_t)16 * F * F + (size_t)8 * (F / 16) * 64 * 4;
     T->ubytes = ufl * sizeof(float);
