@@ -243,21 +243,22 @@ wgrad_f32_kernel(const float* __restrict__ X, int ldx, int K, const float* __res
 // are loaded into registers beside the current board's MFMAs.  partial[split][xi][ci][co]; every
 // element sums its split's rows in row order (fixed order; splits reduced in order by
 // wino_wgrad_reduce_out_kernel).
-constexpr int WG_S = 256 + 16;
+// LDS row strides (floats): V rows are read by ds_read_b128 (lane groups {0-3,12-15,20-27}, ...:
+// two rows per group, conflict-free when the rows are 0 mod 64 banks apart), M' rows by
+// ds_read_b32 (32-lane groups over two rows, conflict-free when 16 mod 32 apart).  One stride of
+// 272 for both measured 36 % of LDS cycles as bank conflicts (profiles/r04g_pmc_train_wino_wgrad_gemm.json).
+constexpr int WG_SX = 256, WG_SD = 256 + 16;
 // the four F(2x2,3x3) combinations: (a, b) = (e0, e2) / (e1, e2) / (e1, e2) / (e1, e3) of a patch
 // row or column -> a - b, a + b, b - a, a - b (B^T rows)
 __device__ __forceinline__ f32x4 wino_comb(int k, f32x4 a, f32x4 b) { return k == 1 ? a + b : k == 2 ? b - a : a - b; }
-// NWG waves: 8 (wave w owns co [32 w, 32 w + 32), two tiles staged per thread) or 16 (co [16 w,
-// 16 w + 16), one tile per thread, 4 waves per SIMD at <= 128 VGPRs); every dU element takes the
-// same MFMAs in the same order either way (bit-identical).
-template <int NWG>
-__global__ void __launch_bounds__(NWG * 64)
+// (16 waves of 16 output channels each, 4 per SIMD at <= 128 VGPRs, measured the same: 166.1 vs
+// 166.7 us, profiles/r04g_train_kernel_stats_w16.csv; not kept)
+__global__ void __launch_bounds__(512)
 wino_wgrad_gemm_kernel(const float* __restrict__ X, const float* __restrict__ DY, int K, int rows_per_split,
                        float* __restrict__ partial) {
-    constexpr int F = 256, CO = F / NWG, NN = CO / 16, TPT = 16 / NWG;
-    static_assert(NWG == 8 || NWG == 16, "8 or 16 waves");
-    __shared__ __attribute__((aligned(16))) float xs[16 * WG_S];
-    __shared__ __attribute__((aligned(16))) float ds[16 * WG_S];
+    constexpr int NWG = 8, F = 256, CO = F / NWG, NN = CO / 16, TPT = 16 / NWG;
+    __shared__ __attribute__((aligned(16))) float xs[16 * WG_SX];
+    __shared__ __attribute__((aligned(16))) float ds[16 * WG_SD];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int split = blockIdx.x, xi = blockIdx.y, r = xi >> 2, q = xi & 3;
     const int i1 = r == 0 ? 0 : 1, i2 = r == 3 ? 3 : 2, j1 = q == 0 ? 0 : 1, j2 = q == 3 ? 3 : 2;
@@ -318,8 +319,8 @@ wino_wgrad_gemm_kernel(const float* __restrict__ X, const float* __restrict__ DY
 #pragma unroll
             for (int bb = 0; bb < 2; bb++) p[bb] = yv[u][0][bb] * ra + yv[u][1][bb] * rb;
             const f32x4 m = p[0] * qa + p[1] * qb;
-            *reinterpret_cast<f32x4*>(xs + t * WG_S + c4) = v;
-            *reinterpret_cast<f32x4*>(ds + t * WG_S + c4) = m;
+            *reinterpret_cast<f32x4*>(xs + t * WG_SX + c4) = v;
+            *reinterpret_cast<f32x4*>(ds + t * WG_SD + c4) = m;
         }
         __syncthreads();
         if (rc + 16 < rend) fetch(rc + 16);
@@ -328,10 +329,10 @@ wino_wgrad_gemm_kernel(const float* __restrict__ X, const float* __restrict__ DY
             const int rq = qq * 4 + (lane >> 4);
             float bv[NN];
 #pragma unroll
-            for (int n = 0; n < NN; n++) bv[n] = ds[rq * WG_S + CO * w + 16 * n + (lane & 15)];
+            for (int n = 0; n < NN; n++) bv[n] = ds[rq * WG_SD + CO * w + 16 * n + (lane & 15)];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                const f32x4 a = *reinterpret_cast<const f32x4*>(xs + rq * WG_S + 64 * j + 4 * (lane & 15));
+                const f32x4 a = *reinterpret_cast<const f32x4*>(xs + rq * WG_SX + 64 * j + 4 * (lane & 15));
 #pragma unroll
                 for (int c = 0; c < 4; c++)
 #pragma unroll
@@ -1075,7 +1076,6 @@ struct Trainer {
     // reduction scratch
     float *wpart = nullptr, *cpart = nullptr, *dwtmp = nullptr;
     float* bpart = nullptr;                  // per-board BN partials [Bmax][2][F] (tr::BoardStats)
-    int wgrad_waves = 8;                     // wino_wgrad_gemm_kernel<8 | 16> (AZ_WGRAD_WAVES)
     float* bsum = nullptr;                   // conv bias-grad partials of bn_back4_kernel [grid][2][C]
     size_t bsum_cap = 0;
     size_t wpart_cap = 0, dwtmp_cap = 0;
@@ -1182,10 +1182,7 @@ int launch_wino_wgrad(Trainer* T, const float* X, const float* DY, int B, float*
     if (splits * 16 * (size_t)F * F > T->wpart_cap) return fail("Winograd wgrad: partial buffer too small");
     if ((size_t)B * 64 * F * 4 >= (size_t)0x40000000) return fail("Winograd wgrad: batch too large for 32-bit offsets");
     hipStream_t st = T->st;
-    if (T->wgrad_waves == 16)
-        tr::wino_wgrad_gemm_kernel<16><<<dim3(splits, 16), 1024, 0, st>>>(X, DY, K, WINO_GEMM_ROWS, T->wpart);
-    else
-        tr::wino_wgrad_gemm_kernel<8><<<dim3(splits, 16), 512, 0, st>>>(X, DY, K, WINO_GEMM_ROWS, T->wpart);
+    tr::wino_wgrad_gemm_kernel<<<dim3(splits, 16), 512, 0, st>>>(X, DY, K, WINO_GEMM_ROWS, T->wpart);
     if ((size_t)F * F % 64) return fail("Winograd wgrad: F * F must be a multiple of 64");
     tr::wino_wgrad_reduce_out_kernel<<<(unsigned)((size_t)F * F / 64), 1024, 0, st>>>(T->wpart, splits, F, g);
     return hipGetLastError() == hipSuccess ? 0 : fail("Winograd wgrad launch failed");
@@ -1531,7 +1528,6 @@ int az_trainer_create(int blocks, int filters, const float* weights, size_t n, i
     const int nconv = 1 + 2 * blocks;
     T->wino = F == 256;
     if (const char* e = getenv("AZ_TRAIN_WINOGRAD")) T->wino = T->wino && atoi(e) != 0;
-    if (const char* e = getenv("AZ_WGRAD_WAVES")) T->wgrad_waves = atoi(e) == 16 ? 16 : 8;
     // Winograd U per residual conv: 16 points x F x F + 8 zero ring steps of prefetch pad
     const size_t ufl = (size_t)16 * F * F + (size_t)8 * (F / 16) * 64 * 4;
     T->ubytes = ufl * sizeof(float);

@@ -197,7 +197,7 @@ int main() {
     hipMemcpy(x, hx.data(), hx.size() * 4, hipMemcpyHostToDevice);
     hipMemcpy(d, hd.data(), hd.size() * 4, hipMemcpyHostToDevice);
     azi::tr::wino_wgrad_transform_kernel<<<64, 256>>>(x, d, F, B, vt, mt);
-    azi::tr::wino_wgrad_gemm_kernel<8><<<dim3(1, 16), 512>>>(vt, mt, K, 512, part2);    // the committed GEMM
+    azi::tr::wino_wgrad_gemm_kernel<<<dim3(1, 16), 512>>>(vt, mt, K, 512, part2);    // the committed GEMM
     const int variant = getenv("WGDBG_VARIANT") ? atoi(getenv("WGDBG_VARIANT")) : 0;
     if (variant) dbg::fused_kernel<1><<<dim3(1, 16), 512>>>(x, d, K, 512, part, dump);
     else dbg::fused_kernel<0><<<dim3(1, 16), 512>>>(x, d, K, 512, part, dump);
