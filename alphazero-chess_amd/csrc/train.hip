@@ -324,22 +324,40 @@ wino_wgrad_gemm_kernel(const float* __restrict__ X, const float* __restrict__ DY
         }
         __syncthreads();
         if (rc + 16 < rend) fetch(rc + 16);
-#pragma unroll
-        for (int qq = 0; qq < 4; qq++) {
+        // the operands of row quad qq + 1 are read while the MFMAs of qq run (read just in time,
+        // every 8 MFMAs waited on an LDS round trip: 62 % matrix-pipe busy, PMC)
+        float bA[NN], bB[NN];
+        f32x4 aA[4], aB[4];
+        auto rd = [&](int qq, float (&bv)[NN], f32x4 (&av)[4]) {
             const int rq = qq * 4 + (lane >> 4);
-            float bv[NN];
 #pragma unroll
             for (int n = 0; n < NN; n++) bv[n] = ds[rq * WG_SD + CO * w + 16 * n + (lane & 15)];
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const f32x4 a = *reinterpret_cast<const f32x4*>(xs + rq * WG_SX + 64 * j + 4 * (lane & 15));
+            for (int j = 0; j < 4; j++) av[j] = *reinterpret_cast<const f32x4*>(xs + rq * WG_SX + 64 * j + 4 * (lane & 15));
+        };
+        auto mm = [&](const float (&bv)[NN], const f32x4 (&av)[4]) {
+#pragma unroll
+            for (int j = 0; j < 4; j++)
 #pragma unroll
                 for (int c = 0; c < 4; c++)
 #pragma unroll
                     for (int n = 0; n < NN; n++)
-                        acc[4 * j + c][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c], bv[n], acc[4 * j + c][n], 0, 0, 0);
-            }
-        }
+                        acc[4 * j + c][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j][c], bv[n], acc[4 * j + c][n], 0, 0, 0);
+        };
+        rd(0, bA, aA);
+        rd(1, bB, aB);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(bA, aA);
+        __builtin_amdgcn_sched_barrier(0);
+        rd(2, bA, aA);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(bB, aB);
+        __builtin_amdgcn_sched_barrier(0);
+        rd(3, bB, aB);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(bA, aA);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(bB, aB);
     }
     float* out = partial + ((size_t)split * 16 + xi) * F * F;
 #pragma unroll
