@@ -270,8 +270,9 @@ wino_wgrad_gemm_kernel(const float* __restrict__ X, const float* __restrict__ DY
         for (int n = 0; n < NN; n++) acc[b][n] = f32x4{0.f, 0.f, 0.f, 0.f};
     // staging: thread = (channel quad c4, tiles TPT tp .. TPT tp + TPT - 1).  The squares come in
     // through buffer loads: the lane's channel offset is the only VGPR address, the (wave-uniform)
-    // square offset rides in the SGPR offset, and an off-board square is an offset past the buffer's
-    // end, which the hardware reads as 0 (no branch, no 64-bit address per load)
+    // square offset rides in the SGPR offset, and an off-board square moves the VGPR offset past
+    // the buffer's end (the range check covers the VGPR offset), which the hardware reads as 0 (no
+    // branch, no 64-bit address per load)
     const int c4 = (tid & 63) * 4, tp = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int xbytes = (K >> 4) * 64 * F * 4;   // K (board, tile) rows = K / 16 boards
     const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, xbytes, 0x00020000);
@@ -288,8 +289,9 @@ wino_wgrad_gemm_kernel(const float* __restrict__ X, const float* __restrict__ DY
 #pragma unroll
                 for (int jj = 0; jj < 2; jj++) {
                     const int row = 2 * ty - 1 + (ii ? i2 : i1), col = 2 * tx - 1 + (jj ? j2 : j1);
-                    const int so = ((unsigned)row < 8u && (unsigned)col < 8u) ? bb0 + (row * 8 + col) * F * 4 : OFF_BOARD;
-                    xd[u][ii][jj] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rX, c4 * 4, so, 0));
+                    const bool on = (unsigned)row < 8u && (unsigned)col < 8u;
+                    xd[u][ii][jj] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                  rX, on ? c4 * 4 : OFF_BOARD, on ? bb0 + (row * 8 + col) * F * 4 : 0, 0));
                 }
 #pragma unroll
             for (int a = 0; a < 2; a++)
