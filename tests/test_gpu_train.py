@@ -238,16 +238,24 @@ def test_winograd_training_convs_match_direct(require_gpu, monkeypatch):
 
 def test_winograd_weight_grad_multi_split(require_gpu):
     """the production Winograd weight grad (wino_wgrad_gemm_kernel, 512 rows of
-    (board, tile) per split, the splits summed by reduce_kernel) with more than one split: 80 boards
-    = 1280 rows = 3 splits, the last one partial.  Every gradient tensor against the float64 oracle
-    under the GPU's ReLU masks (1e-4 relative norm), at F = 256 where that kernel runs."""
+    (board, tile) per split, the splits summed by wino_wgrad_reduce_out_kernel) with more than one
+    split: 80 boards = 1280 rows = 3 splits, the last one partial.  Every gradient tensor against
+    the float64 oracle under the GPU's ReLU masks (1e-4 relative norm), at F = 256 where that kernel
+    runs.  The same batch pins the per-board BatchNorm statistics of the Winograd conv epilogues
+    (round 4: forward sums / squared deviations combined over 80 boards, backward dz sums): the
+    BN gamma / beta grads above and the running statistics below."""
     blocks, filters, n = 2, 256, 80
     w = A.random_weights(blocks, filters, seed=13)
     planes, tpol, tval = batch(n, seed=81)
     tr = A.Trainer(blocks, filters, weights=w, max_batch=n)
     tr.compute_gradients(planes, tpol, tval)
     g = tr.grads()
-    rg, _ = T.TrainRef(blocks, filters, w).grads(planes, tpol, tval, tr.relu_masks(n))
+    ref = T.TrainRef(blocks, filters, w)
+    rg, _ = ref.grads(planes, tpol, tval, tr.relu_masks(n))
+    p = tr.params()
+    rs = ref.running_stats_flat(w)
+    stats = ~T.trainable_mask(blocks, filters)
+    assert np.all(np.abs(p[stats] - rs[stats]) <= 1e-5 * (1 + np.abs(rs[stats])))
     seg, _ = T.segments(blocks, filters)
     zero_bias = bn_fed_biases(blocks)
     checked = 0
