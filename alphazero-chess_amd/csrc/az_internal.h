@@ -120,6 +120,7 @@ struct Engine {
     float* c_pri;                          // [slots][MAX_EDGES]
     float* cached_value;                   // [G] value of a cache-served leaf
     unsigned long long* g_sims;            // [G] simulations backed up (summed at readout)
+    unsigned long long* g_evals;           // [G] network rows of the persistent kernel (summed at readout)
     unsigned long long* g_sel_bytes;       // [G] algorithmic bytes read by k_select
     unsigned long long* trace;             // [G][8] s_memtime phase stamps of k_step (AZ_STEP_TRACE builds only)
     // evaluation log

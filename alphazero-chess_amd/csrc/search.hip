@@ -684,7 +684,6 @@ int run_sims(az_search* s, int i0 = 0, int i1 = -1) {
             while (j < i1 && !(tm && j % TIMING_EVERY == 0)) j++;
             if (pending >= 0) k_backup<<<(s->E.G * 64 + 255) / 256, 256, 0, s->st>>>(s->E, pending);
             pending = -1;
-            AZ_HIP(hipMemsetAsync(s->E.batch_hist + i, 0, (size_t)(j - i) * sizeof(int), s->st));
             rc = sims_persistent(s->net->dev, s->E, s->so, i, j, s->st);
             if (rc) return rc;
             i = j - 1;
@@ -915,7 +914,7 @@ int az_search_create(az_net* net, const az_search_cfg* cfg, int device, az_searc
     rc |= dalloc(s, &E.ctr, 1);
     rc |= dalloc(s, &E.batch_hist, S);
     rc |= dalloc(s, &E.cached_value, G);
-    rc |= dalloc(s, &E.g_sims, G); rc |= dalloc(s, &E.g_sel_bytes, G);
+    rc |= dalloc(s, &E.g_sims, G); rc |= dalloc(s, &E.g_sel_bytes, G); rc |= dalloc(s, &E.g_evals, G);
 #ifdef AZ_STEP_TRACE
     rc |= dalloc(s, &E.trace, (size_t)G * 16);
 #endif
@@ -1067,6 +1066,7 @@ int az_selfplay_reset(az_search* s) {
     if (rc) return rc;
     AZ_HIP(hipMemset(s->E.ctr, 0, sizeof(Counters)));
     AZ_HIP(hipMemset(s->E.g_sims, 0, (size_t)s->E.G * 8));
+    AZ_HIP(hipMemset(s->E.g_evals, 0, (size_t)s->E.G * 8));
     if (s->E.cache_mask >= 0) AZ_HIP(hipMemset(s->E.c_state, 0, (size_t)(s->E.cache_mask + 1) * sizeof(unsigned)));
     const int G = s->E.G;
     AZ_HIP(hipMemcpy(&s->E.ctr->next_game_id, &G, 4, hipMemcpyHostToDevice));
@@ -1141,13 +1141,14 @@ int az_search_stats_get(az_search* s, az_search_stats* out) {
     Counters c;
     AZ_HIP(hipMemcpy(&c, s->E.ctr, sizeof(c), hipMemcpyDeviceToHost));
     out->sims = (int64_t)(c.sims + sum_games(s, s->E.g_sims));
-    out->evals = (int64_t)c.evals;
+    const unsigned long long ge = sum_games(s, s->E.g_evals);
+    out->evals = (int64_t)(c.evals + ge);
     out->terminal_leaves = (int64_t)c.terminal;
     out->games_finished = (int64_t)c.games_finished;
     out->moves = (int64_t)c.moves;
     out->max_depth_sum = (int64_t)c.depth_sum;
     out->cache_hits = (int64_t)c.cache_hits;
-    out->cache_misses = (int64_t)c.evals;
+    out->cache_misses = (int64_t)(c.evals + ge);
     out->overflow = c.overflow;
     std::vector<int> nc(s->E.G), ec(s->E.G);
     AZ_HIP(hipMemcpy(nc.data(), s->E.node_count, s->E.G * 4, hipMemcpyDeviceToHost));

@@ -1154,8 +1154,10 @@ k_sims32w(Engine E, TowerArgs ta, SearchOut so, int step0, int step1) {
                         E.row_game[g] = g;
                         E.row_node[g] = nid;
                         E.leaf_row[g] = g;
-                        atomicAdd(&E.batch_hist[step], 1);
-                        atomicAdd(&E.ctr->evals, 1ull);
+                        // per-game slot, summed at readout: two same-address atomics from every
+                        // workgroup per simulation were waited on at the barrier below (batch_hist
+                        // is read only for the timed steps, which never run in this kernel)
+                        E.g_evals[g] += 1ull;   // g is in a VGPR: a vector load, never the scalar cache
                     } else if (kind == X_TERMINAL) {
                         atomicAdd(&E.ctr->terminal, 1ull);
                     } else if (kind == X_CACHED) {
