@@ -272,23 +272,6 @@ __device__ __forceinline__ void heads_group(const char* __restrict__ xb, float* 
     // f32 with 4 waves: A's first KA 16-channel weight groups are requested before everything else,
     // so that the 1x1 conv does not wait behind the B / C prefetch
     constexpr int KA = (F32X && NW <= 4) ? (F / 16 < 4 ? F / 16 : 4) : 0;
-    // Loads in the order their phases use them: the vmcnt counter is in order, so a phase that waits
-    // for its own operands then does not also wait for the value-FC rows behind them (128 KB per
-    // board at F = 64, ~2k cycles of L2 -> CU transfer); those stream in during A and B.  (Round 3
-    // issued the biases and the new node's record after the value-FC rows: A's epilogue and the
-    // record's dependent load waited for the whole stream, 7.7k cycles of A at C2.)
-    int sgame[NB], snode[NB];
-    Node snd[NB];
-    if constexpr (SEARCH) {                             // the row's game and node first: the record
-#pragma unroll                                          // load below depends on them
-        for (int bb = 0; bb < NB; bb++) {
-            if (b0 + bb < nb) {
-                const int row = vgpr_index(row0 + b0 + bb);
-                sgame[bb] = so.row_game[row];
-                snode[bb] = so.row_node[row];
-            }
-        }
-    }
     f32x4 hA[KA > 0 ? KA : 1][3];
     if constexpr (KA > 0) {
         if (w < 4 * NB) {
@@ -298,9 +281,6 @@ __device__ __forceinline__ void heads_group(const char* __restrict__ xb, float* 
                 for (int cf = 0; cf < 3; cf++) hA[kc][cf] = __builtin_bit_cast(f32x4, hfrag[(kc * 3 + cf) * 64 + lane]);
         }
     }
-    f32x4 b40v[3];
-#pragma unroll
-    for (int cf = 0; cf < 3; cf++) b40v[cf] = *reinterpret_cast<const f32x4*>(head + L.b40 + cf * 16 + 4 * h);
     float pa[TPW > 0 ? TPW : 1][8];
 #pragma unroll
     for (int k = 0; k < TPW; k++) {
@@ -318,11 +298,6 @@ __device__ __forceinline__ void heads_group(const char* __restrict__ xb, float* 
             for (int ks = 0; ks < 8; ks++) pa[k][ks] = head[L.p2w + (cf * 16 + l16) * 32 + h + ks * 4];
         }
     }
-    f32x4 p2bv[TPW > 0 ? TPW : 1];
-#pragma unroll
-    for (int k = 0; k < TPW; k++)
-        p2bv[k] = *reinterpret_cast<const f32x4*>(head + L.p2b + ((w + k * NW) >> 2 & 3) * 16 + 4 * h);
-    const float l1bv = head[L.l1b + lane], l2wv = head[L.l2w + lane], l2bv = head[L.l2b];
     float wv[KPRE > 0 && !WIDE ? KPRE : 1];
     f32x4 wq[WIDE ? KP / 4 : 1];
     if constexpr (WIDE) {
@@ -333,10 +308,29 @@ __device__ __forceinline__ void heads_group(const char* __restrict__ xb, float* 
 #pragma unroll
         for (int i = 0; i < KPRE; i++) wv[i] = head[L.l1w + (size_t)(w * KP + i) * 64 + lane];
     }
-    if constexpr (SEARCH) {                             // the new node's record (used after the softmax)
+    // biases of A, B and the value head, and (search mode) the new node's record: requested here,
+    // behind the weight prefetches, so that no phase ends on a dependent global load (C2 heads
+    // stamps: ~1-2k cycles each)
+    f32x4 b40v[3];
 #pragma unroll
-        for (int bb = 0; bb < NB; bb++)
-            if (b0 + bb < nb) snd[bb] = so.nodes[(size_t)sgame[bb] * so.NMAX + snode[bb]];
+    for (int cf = 0; cf < 3; cf++) b40v[cf] = *reinterpret_cast<const f32x4*>(head + L.b40 + cf * 16 + 4 * h);
+    f32x4 p2bv[TPW > 0 ? TPW : 1];
+#pragma unroll
+    for (int k = 0; k < TPW; k++)
+        p2bv[k] = *reinterpret_cast<const f32x4*>(head + L.p2b + ((w + k * NW) >> 2 & 3) * 16 + 4 * h);
+    const float l1bv = head[L.l1b + lane], l2wv = head[L.l2w + lane], l2bv = head[L.l2b];
+    int sgame[NB], snode[NB];
+    Node snd[NB];
+    if constexpr (SEARCH) {
+#pragma unroll
+        for (int bb = 0; bb < NB; bb++) {
+            if (b0 + bb < nb) {
+                const int row = vgpr_index(row0 + b0 + bb);
+                sgame[bb] = so.row_game[row];
+                snode[bb] = so.row_node[row];
+                snd[bb] = so.nodes[(size_t)sgame[bb] * so.NMAX + snode[bb]];
+            }
+        }
     }
     // A
     for (int sfr = w; sfr < 4 * NB; sfr += NW) {
