@@ -214,7 +214,8 @@ wgrad_f32_kernel(const float* __restrict__ X, int ldx, int K, const float* __res
                 const int base = ok ? src * GS : GR * GS;
 #pragma unroll
                 for (int i = 0; i < 4; i++)
-                    acc[t][i] = __builtin_amdgcn_mfma_f32_16x16x4f32(xs[base + i * 16 + (lane & 15)], b, acc[t][i], 0, 0, 0);
+                    if (k0 + i * 16 < K)   // (uniform) K < 64: the input conv's 32 channels
+                        acc[t][i] = __builtin_amdgcn_mfma_f32_16x16x4f32(xs[base + i * 16 + (lane & 15)], b, acc[t][i], 0, 0, 0);
             }
         }
     }
@@ -686,11 +687,14 @@ __global__ void __launch_bounds__(256) bn_back4_kernel(const float* __restrict__
     }
 }
 
-// planes [B][19][64] (to_tensor layout, chess.rs:191-245) -> X0 [B*64][64] (channels >= 19 zero)
+// planes [B][19][64] (to_tensor layout, chess.rs:191-245) -> X0 [B*64][X0C] (channels >= 19 zero;
+// X0C = 32, the smallest multiple of the convs' 16-channel K chunk: the input conv and its weight
+// grad ran on 64 padded channels before round 4, 3.4x the 19 real ones)
+constexpr int X0C = 32;
 __global__ void planes_kernel(const float* __restrict__ planes, int B, float* __restrict__ x0) {
-    const size_t n = (size_t)B * 64 * 64;
+    const size_t n = (size_t)B * 64 * X0C;
     for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
-        const int c = (int)(e & 63), r = (int)(e >> 6), b = r >> 6, s = r & 63;
+        const int c = (int)(e % X0C), r = (int)(e / X0C), b = r >> 6, s = r & 63;
         x0[e] = c < 19 ? planes[((size_t)b * 19 + c) * 64 + s] : 0.0f;
     }
 }
@@ -1085,7 +1089,7 @@ struct Trainer {
     size_t ubytes = 0;
     float *w40f = nullptr, *w40d = nullptr, *b40 = nullptr, *wp2f = nullptr, *w1d = nullptr;
     // saved activations (R = B*64 rows)
-    float* x0 = nullptr;                     // [R][64] input planes
+    float* x0 = nullptr;                     // [R][X0C] input planes
     std::vector<float*> xs, y1, hh, y2;      // xs[0..blocks], y1/hh/y2[blocks]
     float *y0 = nullptr, *y40 = nullptr, *a40 = nullptr, *logits = nullptr, *vflat = nullptr, *h1 = nullptr;
     // gradients of activations
@@ -1317,7 +1321,7 @@ int trainer_grads(Trainer* T, const float* planes, const float* tpol, const floa
     for (size_t i = 0; i < L.tower.size(); i++) {
         const auto& c = L.tower[i];
         if (i > 0 && T->wino) continue;
-        const int kpad = i == 0 ? 64 : F;
+        const int kpad = i == 0 ? tr::X0C : F;
         tr::repack3x3_kernel<<<grid_for((size_t)9 * kpad * F), 256, 0, st>>>(T->p + c.w, F, c.cin, kpad, T->wf[i],
                                                                            i == 0 ? nullptr : T->wd[i]);
     }
@@ -1336,8 +1340,8 @@ int trainer_grads(Trainer* T, const float* planes, const float* tpol, const floa
     tr::transpose_kernel<<<grid_for(512 * 64), 256, 0, st>>>(T->p + L.l1w, 512, 64, T->w1d, 512, 64);
 
     // ---------------- forward (agent.rs:112-144, training-mode BatchNorm)
-    tr::planes_kernel<<<grid_for((size_t)R * 64), 256, 0, st>>>(T->planes, B, T->x0);
-    TRY(launch_conv(T, 9, T->x0, 64, 64, T->wf[0], F, T->p + L.tower[0].b, nullptr, T->y0, F, R));
+    tr::planes_kernel<<<grid_for((size_t)R * tr::X0C), 256, 0, st>>>(T->planes, B, T->x0);
+    TRY(launch_conv(T, 9, T->x0, tr::X0C, tr::X0C, T->wf[0], F, T->p + L.tower[0].b, nullptr, T->y0, F, R));
     TRY(bn_forward(T, 0, T->y0, F, F, R, L.tower[0].bn, nullptr, T->xs[0]));
     for (int b = 0; b < T->blocks; b++) {
         const auto& c1 = L.tower[1 + 2 * b];
@@ -1434,8 +1438,8 @@ int trainer_grads(Trainer* T, const float* planes, const float* tpol, const floa
     // input conv (no data grad)
     TRY(bn_backward(T, 0, T->dx, T->xs[0], T->y0, F, F, R, L.tower[0].bn, T->dy, nullptr, dx_stats ? T->bpart : nullptr,
                     T->g + L.tower[0].b));
-    TRY(launch_wgrad(T, 9, T->x0, 64, 64, T->dy, F, F, R, T->dwtmp, T->dwtmp_cap));
-    tr::unpack3x3_kernel<<<grid_for((size_t)9 * 19 * F), 256, 0, st>>>(T->dwtmp, F, 19, 64, T->g + L.tower[0].w);
+    TRY(launch_wgrad(T, 9, T->x0, tr::X0C, tr::X0C, T->dy, F, F, R, T->dwtmp, T->dwtmp_cap));
+    tr::unpack3x3_kernel<<<grid_for((size_t)9 * 19 * F), 256, 0, st>>>(T->dwtmp, F, 19, tr::X0C, T->g + L.tower[0].w);
     AZ_HIP(hipMemcpyAsync(T->hloss, T->loss, (size_t)B * 2 * sizeof(float), hipMemcpyDeviceToHost, st));
     AZ_HIP(hipStreamSynchronize(st));
     if (losses) {   // training.rs:281-282: means over the batch (policy, value)
@@ -1554,13 +1558,13 @@ int az_trainer_create(int blocks, int filters, const float* weights, size_t n, i
     if (T->wino && nconv > 1) T->ubase = A(2 * (size_t)(nconv - 1) * ufl);
     for (int i = 0; i < nconv; i++) {
         const bool w9 = i == 0 || !T->wino;
-        T->wf.push_back(w9 ? A((size_t)9 * (i == 0 ? 64 : F) * F) : nullptr);
+        T->wf.push_back(w9 ? A((size_t)9 * (i == 0 ? tr::X0C : F) * F) : nullptr);
         T->wd.push_back(i == 0 || !w9 ? nullptr : A((size_t)9 * F * F));
         T->uf.push_back(i > 0 && T->ubase ? T->ubase + (size_t)(2 * (i - 1)) * ufl : nullptr);
         T->ud.push_back(i > 0 && T->ubase ? T->ubase + (size_t)(2 * (i - 1) + 1) * ufl : nullptr);
     }
     T->w40f = A((size_t)F * 64); T->w40d = A((size_t)64 * F); T->b40 = A(64); T->wp2f = A(32 * 64); T->w1d = A(64 * 512);
-    T->x0 = A(R * 64);
+    T->x0 = A(R * tr::X0C);
     for (int b = 0; b <= blocks; b++) T->xs.push_back(A(R * F));
     for (int b = 0; b < blocks; b++) { T->y1.push_back(A(R * F)); T->hh.push_back(A(R * F)); T->y2.push_back(A(R * F)); }
     T->y0 = A(R * F); T->y40 = A(R * 64); T->a40 = A(R * 64); T->logits = A(R * 64);
