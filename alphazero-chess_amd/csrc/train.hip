@@ -214,8 +214,7 @@ wgrad_f32_kernel(const float* __restrict__ X, int ldx, int K, const float* __res
                 const int base = ok ? src * GS : GR * GS;
 #pragma unroll
                 for (int i = 0; i < 4; i++)
-                    if (k0 + i * 16 < K)   // (uniform) K < 64: the input conv's 32 channels
-                        acc[t][i] = __builtin_amdgcn_mfma_f32_16x16x4f32(xs[base + i * 16 + (lane & 15)], b, acc[t][i], 0, 0, 0);
+                    acc[t][i] = __builtin_amdgcn_mfma_f32_16x16x4f32(xs[base + i * 16 + (lane & 15)], b, acc[t][i], 0, 0, 0);
             }
         }
     }
@@ -688,8 +687,10 @@ __global__ void __launch_bounds__(256) bn_back4_kernel(const float* __restrict__
 }
 
 // planes [B][19][64] (to_tensor layout, chess.rs:191-245) -> X0 [B*64][X0C] (channels >= 19 zero;
-// X0C = 32, the smallest multiple of the convs' 16-channel K chunk: the input conv and its weight
-// grad ran on 64 padded channels before round 4, 3.4x the 19 real ones)
+// X0C = 32, the smallest multiple of the convs' 16-channel K chunk: the input conv ran on 64 padded
+// channels before round 4, 3.4x the 19 real ones -- 96 -> 56 us per step.  Its weight grad keeps its
+// 64-wide k tile (skipping the empty half with a uniform branch around the MFMAs measured slower,
+// and slowed the 1-tap instantiation 2x))
 constexpr int X0C = 32;
 __global__ void planes_kernel(const float* __restrict__ planes, int B, float* __restrict__ x0) {
     const size_t n = (size_t)B * 64 * X0C;
