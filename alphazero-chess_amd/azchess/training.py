@@ -157,18 +157,18 @@ class Trainer:
     def compute_gradients(self, planes, tpol, tval):
         planes, tpol, tval = self._batch(planes, tpol, tval)
         loss = np.zeros(2, np.float32)
-        L.check(L.lib.az_trainer_compute_grads(self._h, L.fptr(planes), L.fptr(tpol), L.fptr(tval),
-                                               planes.shape[0], L.fptr(loss)))
+        self._check(L.lib.az_trainer_compute_grads(self._h, L.fptr(planes), L.fptr(tpol), L.fptr(tval),
+                                                   planes.shape[0], L.fptr(loss)))
         return float(loss[0]), float(loss[1])
 
     def apply(self, lr):
-        L.check(L.lib.az_trainer_apply(self._h, float(lr)))
+        self._check(L.lib.az_trainer_apply(self._h, float(lr)))
 
     def step(self, planes, tpol, tval, lr):
         planes, tpol, tval = self._batch(planes, tpol, tval)
         loss = np.zeros(2, np.float32)
-        L.check(L.lib.az_trainer_step(self._h, L.fptr(planes), L.fptr(tpol), L.fptr(tval), planes.shape[0],
-                                      float(lr), L.fptr(loss)))
+        self._check(L.lib.az_trainer_step(self._h, L.fptr(planes), L.fptr(tpol), L.fptr(tval), planes.shape[0],
+                                          float(lr), L.fptr(loss)))
         return float(loss[0]), float(loss[1])
 
     def params(self):
@@ -201,6 +201,17 @@ class Trainer:
                 out.append(a.reshape(batch, 64) > 0)
         return out
 
+    _pending = None
+
+    def _check(self, rc):
+        """L.check for calls that may run the host reducer: a KeyboardInterrupt / SystemExit raised
+        inside it is re-raised here, after the C call has returned its error."""
+        e = self._pending[0] if self._pending else None
+        if e is not None:
+            self._pending[0] = None
+            raise e
+        return L.check(rc)
+
     def set_comm(self, unique_id, rank, world):
         buf = (C.c_char * 128).from_buffer_copy(unique_id)
         L.check(L.lib.az_trainer_set_comm(self._h, buf, int(rank), int(world)))
@@ -213,13 +224,22 @@ class Trainer:
             try:
                 reduce(np.ctypeslib.as_array(ptr, shape=(n,)))
                 return 0
-            except BaseException:            # nothing may unwind through the C frames
-                import traceback
-                traceback.print_exc()
+            except BaseException as e:       # nothing may unwind through the C frames; a
+                import traceback             # KeyboardInterrupt / SystemExit is re-raised by
+                traceback.print_exc()        # _check once the C call has returned (as tree.py)
+                if not isinstance(e, Exception):
+                    self._pending[0] = e
                 return 1
+        self._pending = [None]
         self._reduce_fn = L.ALLREDUCE_FN(fn)   # kept alive with the trainer
         L.check(L.lib.az_trainer_set_host_reducer(self._h, C.cast(self._reduce_fn, C.c_void_p), None, int(rank),
                                                   int(world)))
+
+    def set_sharded(self, on=True):
+        """Sharded batch (az_trainer_set_sharded): this rank's batches are its shard of one global
+        batch -- the reference's single 512 step (training.rs:137-159) split over the ranks, with
+        BatchNorm statistics, the BN backward and the loss over the whole global batch."""
+        L.check(L.lib.az_trainer_set_sharded(self._h, int(bool(on))))
 
     def timing(self, reset=False):
         """(step_ms, allreduce_ms, steps): device time summed over the steps since the last reset."""
@@ -236,20 +256,29 @@ class Trainer:
 
 def train(iterations, blocks=NUM_RES_BLOCKS, filters=NUM_FILTERS, games=NUM_EPISODES, sims=NUM_SIMULATIONS,
           min_replay=MIN_REPLAY_SIZE, train_steps=NUM_TRAIN_STEPS, batch_size=BATCH_SIZE, replay=None, trainer=None,
-          device=0, seed=SEED, dtype="f32", comm=None, log=None):
+          device=0, seed=SEED, dtype="f32", comm=None, shard_batch=False, log=None):
     """train() (training.rs:39-275) without the TUI, arena and Elo (SKIP_VALIDATION = true,
     parameters.rs:35): per iteration, self-play `games` games with model.valid() until the replay
     buffer holds min_replay unique positions, then train_steps AdamW steps on batches of
     batch_size at get_cyclical_lr(iteration); the new model replaces the old one.
     comm = (unique_id, rank, world) makes the gradient step data-parallel over RCCL: every rank
-    plays its own games (seed offset by rank) into its own buffer.
+    plays its own games (seed offset by rank) into its own buffer.  shard_batch (with comm): each
+    step is the reference's ONE batch of batch_size split over the ranks (batch_size / world per
+    rank, az_trainer_set_sharded: BatchNorm statistics over the whole batch); without it every
+    rank trains its own batch_size (global batch batch_size x world, per-rank BatchNorm).
     Returns (trainer, replay, per-iteration stats)."""
     from .memory import ReplayBuffer
     rank = comm[1] if comm else 0
+    world = comm[2] if comm else 1
+    if shard_batch and batch_size % world:
+        raise ValueError("shard_batch: batch_size %d is not a multiple of world %d" % (batch_size, world))
+    local_batch = batch_size // world if shard_batch else batch_size
     if trainer is None:
-        trainer = Trainer(blocks, filters, max_batch=batch_size, device=device, seed=seed)
+        trainer = Trainer(blocks, filters, max_batch=local_batch, device=device, seed=seed)
         if comm:
             trainer.set_comm(*comm)
+        if shard_batch:
+            trainer.set_sharded(True)
     replay = replay if replay is not None else ReplayBuffer()
     history = []
     for iteration in range(iterations):
@@ -279,7 +308,7 @@ def train(iterations, blocks=NUM_RES_BLOCKS, filters=NUM_FILTERS, games=NUM_EPIS
         lr = get_cyclical_lr(iteration)
         pl_sum = vl_sum = 0.0
         for b in range(train_steps):
-            planes, pol, val, _ = replay.sample_arrays(batch_size, seed=(seed << 20) ^ (iteration << 8) ^ b ^ rank << 40)
+            planes, pol, val, _ = replay.sample_arrays(local_batch, seed=(seed << 20) ^ (iteration << 8) ^ b ^ rank << 40)
             pl, vl = trainer.step(planes, pol, val, lr)
             pl_sum += pl
             vl_sum += vl

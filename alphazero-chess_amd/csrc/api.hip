@@ -111,11 +111,9 @@ int az_pos_from_fen(const char* fen, az_pos* out) {
     p.halfmoves = (uint16_t)hm;
     p.fullmoves = (uint16_t)(fm < 1 ? 1 : fm);
     p.ep = azc::pseudo_ep(p, ep);
-    if (__builtin_popcountll(p.bb[azc::KING] & p.bb[azc::WHITE_BB]) != 1 ||
-        __builtin_popcountll(p.bb[azc::KING] & p.bb[azc::BLACK_BB]) != 1)
-        return fail("FEN must have one king per side");
     bool chk;
     azc::finalize(p, &chk);
+    if (const char* why = azc::setup_error(p)) return fail(std::string("FEN rejected (") + why + "): " + fen);
     P(out) = p;
     return 0;
 }

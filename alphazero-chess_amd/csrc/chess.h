@@ -424,6 +424,63 @@ AZ_HD int finalize(Pos& p, bool* in_check) {
     return n;
 }
 
+// Why a caller's position is not one shakmaty's Chess::from_setup accepts (its PositionErrorKinds:
+// bitboard consistency, one king per side, too much material, pawns on a back rank, invalid
+// castling rights / ep square, the side not to move in check, impossible check), or nullptr.
+// The reference only ever reaches positions by legal play from Chess::default() (training.rs:344),
+// so these are exactly the positions it can hold; the engine sizes a node's edges for 218 legal
+// moves (az_internal.h MAX_EDGES, search.hip EMAX), which every accepted position respects.
+inline const char* setup_error(const Pos& p) {
+    const uint64_t w = p.bb[WHITE_BB], b = p.bb[BLACK_BB];
+    if (w & b) return "white and black bitboards overlap";
+    uint64_t roles = 0;
+    for (int r = 0; r < 6; r++) {
+        if (roles & p.bb[r]) return "piece bitboards overlap";
+        roles |= p.bb[r];
+    }
+    if (roles != (w | b)) return "piece and colour bitboards disagree";
+    if (p.turn > 1 || p.castling > 15) return "bad turn or castling field";
+    for (int c = 0; c < 2; c++) {
+        const uint64_t s = c ? b : w;
+        if (popc64(p.bb[KING] & s) != 1) return "each side needs exactly one king";
+        const int pawns = popc64(p.bb[PAWN] & s);
+        if (popc64(s) > 16 || pawns > 8) return "too much material";
+        const int extra = (popc64(p.bb[QUEEN] & s) > 1 ? popc64(p.bb[QUEEN] & s) - 1 : 0) +
+                          (popc64(p.bb[ROOK] & s) > 2 ? popc64(p.bb[ROOK] & s) - 2 : 0) +
+                          (popc64(p.bb[BISHOP] & s) > 2 ? popc64(p.bb[BISHOP] & s) - 2 : 0) +
+                          (popc64(p.bb[KNIGHT] & s) > 2 ? popc64(p.bb[KNIGHT] & s) - 2 : 0);
+        if (extra > 8 - pawns) return "too much material";
+    }
+    if (p.bb[PAWN] & BACKRANKS) return "pawns on a back rank";
+    auto has = [&](int role, uint64_t side, int sq) { return (p.bb[role] & side & (1ULL << sq)) != 0; };
+    if ((p.castling & 3) && !has(KING, w, 4)) return "invalid castling rights";
+    if (((p.castling & 1) && !has(ROOK, w, 7)) || ((p.castling & 2) && !has(ROOK, w, 0))) return "invalid castling rights";
+    if ((p.castling & 12) && !has(KING, b, 60)) return "invalid castling rights";
+    if (((p.castling & 4) && !has(ROOK, b, 63)) || ((p.castling & 8) && !has(ROOK, b, 56))) return "invalid castling rights";
+    const uint64_t occ = w | b, empty = ~occ;
+    if (p.ep < 64) {
+        const int ep = p.ep, fwd = p.turn ? 8 : -8;   // the pushed pawn stands one rank beyond ep
+        const uint64_t them = p.turn ? w : b;
+        if ((ep >> 3) != (p.turn ? 2 : 5) || (occ & (1ULL << ep)) || (occ & (1ULL << (ep - fwd))) ||
+            !(p.bb[PAWN] & them & (1ULL << (ep + fwd))) || pseudo_ep(p, ep) != ep)
+            return "invalid en-passant square";
+    } else if (p.ep != 64) {
+        return "invalid en-passant square";
+    }
+    auto attackers_of = [&](int color) {   // pieces of !color attacking color's king
+        const uint64_t kbb = p.bb[KING] & (color ? b : w), th = color ? w : b;
+        return (pawn_att(color, kbb) & p.bb[PAWN] & th) | (knight_att(kbb) & p.bb[KNIGHT] & th) |
+               (king_att(kbb) & p.bb[KING] & th) | (bishop_att(kbb, empty) & (p.bb[BISHOP] | p.bb[QUEEN]) & th) |
+               (rook_att(kbb, empty) & (p.bb[ROOK] | p.bb[QUEEN]) & th);
+    };
+    if (attackers_of(p.turn ^ 1)) return "the side not to move is in check";
+    if (popc64(attackers_of(p.turn)) > 2) return "impossible check";
+    Pos q = p;
+    bool chk;
+    if (finalize(q, &chk) > 218) return "more than 218 legal moves";
+    return nullptr;
+}
+
 AZ_HD Pos startpos() {
     Pos p;
     p.bb[PAWN] = 0x00FF00000000FF00ULL;

@@ -77,6 +77,10 @@ extern "C" int az_rules_probe(int device, const az_pos* parent, const int32_t* a
     if (n == 0) return 0;
     // the kernels only ever play legal moves: refuse anything else here, on the host
     for (int i = 0; i < n; i++) {
+        // the device scratch holds MAX_EDGES moves: a parent shakmaty would refuse (many queens,
+        // overlapping bitboards, the side not to move in check ...) is refused here too
+        if (const char* why = azc::setup_error(*reinterpret_cast<const azc::Pos*>(parent + i)))
+            return fail("az_rules_probe: item " + std::to_string(i) + ": parent rejected: " + why);
         if (action[i] < 0) continue;
         int32_t lst[AZ_MAX_MOVES];
         const int nl = az_pos_legal_indices(parent + i, lst, AZ_MAX_MOVES);

@@ -760,9 +760,8 @@ int upload_histories(az_search* s, const az_pos* start, const int32_t* hist, con
             p = *reinterpret_cast<const azc::Pos*>(start + g);
             bool chk;
             azc::finalize(p, &chk);          // flags / rep_key from the position itself
-            const uint64_t kings = p.bb[azc::KING];
-            if (__builtin_popcountll(kings & p.bb[azc::WHITE_BB]) != 1 || __builtin_popcountll(kings & p.bb[azc::BLACK_BB]) != 1)
-                return fail("root start position of game " + std::to_string(g) + " needs one king per side");
+            if (const char* why = azc::setup_error(p))
+                return fail("root start position of game " + std::to_string(g) + " rejected: " + why);
         }
         std::vector<azc::Pos> H{p};
         const int b = off ? off[g] : 0, e = off ? off[g + 1] : 0;

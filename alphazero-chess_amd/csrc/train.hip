@@ -564,6 +564,62 @@ __global__ void bn_board_var_kernel(const float* __restrict__ part, int nb, int 
     rmean[c] = rmean[c] * 0.9f + mu * 0.1f;
     rvar[c] = rvar[c] * 0.9f + var * 0.1f;
 }
+// Sharded batch (az_trainer_set_sharded): one global batch split over the ranks, BatchNorm
+// statistics over all of it (burn BatchNorm on the reference's single 512 batch, agent.rs:37,41,
+// training.rs:159).  Each rank writes its slot of a [world][2 slot + 1] exchange buffer -- the sum
+// S[c] of its rows, the squared deviations M2[c] from its OWN mean, and its row count n -- the
+// buffer (zero outside the slot) is summed over ranks (an all-gather through the sum all-reduce,
+// exact: x + 0 = x), and bn_global_kernel combines the slots in rank order with Chan et al.'s
+// pairwise update.  At world = 1 every value is bit-identical to bn_board_var_kernel /
+// finalize_var_kernel: S / n is the same division, the rank's deviation term is exactly 0.
+// bn_local_kernel: the slot from per-board partials (BoardStats STATS 1), the arithmetic of
+// bn_board_var_kernel up to its mean and m2.
+__global__ void bn_local_kernel(const float* __restrict__ part, int nb, int C, int R, float* __restrict__ slot,
+                                int sstride) {
+    FIN_CHANNEL();
+    const float s = part_sum(part, nb, C, c, 0, lane);
+    const float mu = s / (float)R;
+    float m2 = 0.0f;
+    for (int b = lane; b < nb; b += 64) {
+        const float d = part[((size_t)b * 2) * C + c] / 64.0f - mu;
+        m2 += part[((size_t)b * 2 + 1) * C + c] + 64.0f * (d * d);
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) m2 += __shfl_xor(m2, m, 64);
+    if (lane != 0) return;
+    slot[c] = s;
+    slot[sstride + c] = m2;
+    if (c == 0) slot[2 * sstride] = (float)R;
+}
+__global__ void set_value_kernel(float* __restrict__ p, float v) { *p = v; }
+// the ranks' slots -> batch mean / std and the running statistics (momentum 0.1, as
+// finalize_var_kernel); nglob (BN 0 only): the global row count for the loss and the BN backward
+__global__ void bn_global_kernel(const float* __restrict__ xb, int world, int C, int sstride, float* __restrict__ mean,
+                                 float* __restrict__ stdv, float* __restrict__ rmean, float* __restrict__ rvar,
+                                 float* __restrict__ nglob) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const size_t rs = 2 * (size_t)sstride + 1;
+    float n = 0.0f, s = 0.0f;
+    for (int r = 0; r < world; r++) {
+        n += xb[r * rs + 2 * sstride];
+        s += xb[r * rs + c];
+    }
+    const float mu = s / n;
+    float m2 = 0.0f;
+    for (int r = 0; r < world; r++) {
+        const float nr = xb[r * rs + 2 * sstride];
+        if (nr == 0.0f) continue;
+        const float d = xb[r * rs + c] / nr - mu;
+        m2 += xb[r * rs + sstride + c] + nr * (d * d);
+    }
+    const float var = m2 / n;
+    mean[c] = mu;
+    stdv[c] = sqrtf(var + 1e-5f);
+    rmean[c] = rmean[c] * 0.9f + mu * 0.1f;
+    rvar[c] = rvar[c] * 0.9f + var * 0.1f;
+    if (c == 0 && nglob) *nglob = n;
+}
 #undef FIN_CHANNEL
 
 // column sums (16-byte loads when the channel layout allows it, else the scalar kernel), then the
@@ -629,9 +685,10 @@ __global__ void __launch_bounds__(256) bn_apply4_kernel(const float* __restrict_
 __global__ void bn_back_kernel(const float* __restrict__ dout, const float* __restrict__ O, const float* __restrict__ Y,
                                int ld, int C, int R, const float* __restrict__ mean, const float* __restrict__ stdv,
                                const float* __restrict__ gamma, const float* __restrict__ dgamma,
-                               const float* __restrict__ dbeta, float* __restrict__ dy, float* __restrict__ dres) {
+                               const float* __restrict__ dbeta, float* __restrict__ dy, float* __restrict__ dres,
+                               const float* __restrict__ nglob) {
     const size_t n = (size_t)R * C;
-    const float invR = 1.0f / (float)R;
+    const float invR = 1.0f / (nglob ? *nglob : (float)R);
     for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
         const int r = (int)(e / C), c = (int)(e % C);
         const size_t o = (size_t)r * ld + c;
@@ -648,10 +705,11 @@ __global__ void __launch_bounds__(256) bn_back4_kernel(const float* __restrict__
                                                        const float* __restrict__ mean, const float* __restrict__ stdv,
                                                        const float* __restrict__ gamma, const float* __restrict__ dgamma,
                                                        const float* __restrict__ dbeta, float* __restrict__ dy,
-                                                       float* __restrict__ dres, float* __restrict__ bsum) {
+                                                       float* __restrict__ dres, float* __restrict__ bsum,
+                                                       const float* __restrict__ nglob) {
     const int cq = C / 4, c = 4 * (threadIdx.x % cq), rs = 256 / cq;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);   // bsum: this thread's rows of dy, in order
-    const float invR = 1.0f / (float)R;
+    const float invR = 1.0f / (nglob ? *nglob : (float)R);   // sharded batch: all ranks' rows
     const float4 mu = *reinterpret_cast<const float4*>(mean + c), sd = *reinterpret_cast<const float4*>(stdv + c);
     const float4 ga = *reinterpret_cast<const float4*>(gamma + c), dg = *reinterpret_cast<const float4*>(dgamma + c);
     const float4 db = *reinterpret_cast<const float4*>(dbeta + c);
@@ -721,7 +779,7 @@ __global__ void __launch_bounds__(256)
 loss_kernel(const float* __restrict__ logits, const float* __restrict__ tpol, const float* __restrict__ h1,
             const float* __restrict__ tval, const float* __restrict__ w2, const float* __restrict__ b2, int B,
             float* __restrict__ dlogits, float* __restrict__ dh1, float* __restrict__ loss,
-            float* __restrict__ vpart) {
+            float* __restrict__ vpart, const float* __restrict__ nglob) {
     __shared__ float red[256];
     __shared__ float bc[4];
     const int b = blockIdx.x, t = threadIdx.x;
@@ -751,7 +809,7 @@ loss_kernel(const float* __restrict__ logits, const float* __restrict__ tpol, co
 #pragma unroll
     for (int j = 0; j < 16; j++) { l[j] = expf(l[j] - mx); se += l[j]; }
     se = block_reduce(se, false);
-    const float invB = 1.0f / (float)B;
+    const float invB = 1.0f / (nglob ? *nglob / 64.0f : (float)B);   // sharded: the global batch
     float lp = 0.0f, pg = 0.0f, G[16];
 #pragma unroll
     for (int j = 0; j < 16; j++) {
@@ -1114,6 +1172,12 @@ struct Trainer {
     std::vector<float> host_buf;
     int rank = 0, world = 1;
     uint32_t* stat_idx = nullptr; float* stat_buf = nullptr; int nstat = 0;
+    // sharded batch (az_trainer_set_sharded): BatchNorm statistics, the BN backward sums and the
+    // loss normalisation over every rank's rows; xfwd [world][2 slot + 1] forward exchange,
+    // xback [2 slot] backward exchange, nglob the global row count (device), lossx the losses
+    bool sharded = false;
+    float *xfwd = nullptr, *xback = nullptr, *nglob = nullptr, *lossx = nullptr;
+    int xfwd_world = 0;
     std::vector<void*> allocs;
     // timing (HIP events on the trainer stream): whole steps and the gradient all-reduce
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -1214,6 +1278,34 @@ int launch_wino_wgrad(Trainer* T, const float* X, const float* DY, int B, float*
 }
 
 int nblk_rows(int R) { return (R + tr::CS_ROWS - 1) / tr::CS_ROWS; }
+#define TRY(x) do { if ((x) != 0) return -1; } while (0)
+
+int host_allreduce(Trainer* T, float* d, size_t n, const char* what);
+// sum of n floats at d over the ranks, on the trainer stream: RCCL, the host reducer, or nothing
+// (one rank)
+int exchange(Trainer* T, float* d, size_t n, const char* what) {
+    if (T->comm) {
+        if (ncclAllReduce(d, d, n, ncclFloat, ncclSum, T->comm, T->st) != ncclSuccess)
+            return fail(std::string("ncclAllReduce (") + what + ") failed");
+        return 0;
+    }
+    if (T->host_reduce) return host_allreduce(T, d, n, what);
+    return 0;
+}
+
+// sharded batch: the exchange buffers for the current world (allocated on first use)
+int sharded_buffers(Trainer* T) {
+    if (T->xfwd && T->xfwd_world == T->world) return 0;
+    const size_t n = (size_t)T->world * (2 * T->slot + 1) + 2 * (size_t)T->slot + 8;
+    float* q = T->alloc(n);
+    if (!q) return fail("sharded batch: out of device memory");
+    T->xfwd = q;
+    T->xback = q + (size_t)T->world * (2 * T->slot + 1);
+    T->nglob = T->xback + 2 * T->slot;
+    T->lossx = T->nglob + 4;
+    T->xfwd_world = T->world;
+    return 0;
+}
 
 // the four-channel BN kernels apply: C a power of two in [4, 1024], ld and every pointer 16-byte
 // aligned (the per-channel parameter vectors at channel 0 included: c is a multiple of 4)
@@ -1238,7 +1330,27 @@ int bn_forward(Trainer* T, int bi, const float* Y, int ld, int C, int R, size_t 
     if (C > T->slot) return fail("bn: too many channels");
     float* mean = T->bmean + (size_t)bi * T->slot;
     float* sd = T->bstd + (size_t)bi * T->slot;
-    if (bpart) {
+    if (T->sharded) {   // this rank's slot (sum, squared deviations from its mean, rows), exchange, combine
+        const int ss = T->slot, rs = 2 * ss + 1;
+        float* my = T->xfwd + (size_t)T->rank * rs;
+        AZ_HIP(hipMemsetAsync(T->xfwd, 0, (size_t)T->world * rs * sizeof(float), T->st));
+        if (bpart) {
+            if (R % 64 || ld != C) return fail("bn: board statistics need whole boards");
+            tr::bn_local_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(bpart, R / 64, C, R, my, ss);
+        } else {   // the column sums of the unsharded path: S, the rank's mean, M2 about it
+            const int nb = nblk_rows(R);
+            dim3 g(nb, (C + 63) / 64);
+            tr::launch_colsum<0>(g, T->st, Y, ld, C, R, nullptr, nullptr, nullptr, nullptr, T->cpart,
+                                 {tr::FIN_SUM, my, nullptr, nullptr, nullptr});
+            tr::finalize_mean_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(T->cpart, nb, C, R, mean);
+            tr::launch_colsum<1>(g, T->st, Y, ld, C, R, mean, nullptr, nullptr, nullptr, T->cpart,
+                                 {tr::FIN_SUM, my + ss, nullptr, nullptr, nullptr});
+            tr::set_value_kernel<<<1, 1, 0, T->st>>>(my + 2 * ss, (float)R);
+        }
+        TRY(exchange(T, T->xfwd, (size_t)T->world * rs, "BatchNorm statistics"));
+        tr::bn_global_kernel<<<(C + 255) / 256, 256, 0, T->st>>>(T->xfwd, T->world, C, ss, mean, sd, P + 2 * C,
+                                                                 P + 3 * C, bi == 0 ? T->nglob : nullptr);
+    } else if (bpart) {
         if (R % 64 || ld != C) return fail("bn: board statistics need whole boards");
         tr::bn_board_var_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(bpart, R / 64, C, R, mean, sd, P + 2 * C,
                                                                         P + 3 * C);
@@ -1267,6 +1379,7 @@ int bn_backward(Trainer* T, int bi, const float* dout, const float* O, const flo
     const float* sd = T->bstd + (size_t)bi * T->slot;
     float* dgam = T->g + bn_off;
     float* dbet = T->g + bn_off + C;
+    const float* nglob = T->sharded ? T->nglob : nullptr;
     if (bpart) {
         if (R % 64 || ld != C) return fail("bn: board statistics need whole boards");
         tr::finalize_bnback_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(bpart, R / 64, C, dgam, dbet);
@@ -1276,15 +1389,25 @@ int bn_backward(Trainer* T, int bi, const float* dout, const float* O, const flo
         tr::launch_colsum<2>(g, T->st, dout, ld, C, R, mean, sd, O, Y, T->cpart,
                              {tr::FIN_BNBACK, dgam, dbet, nullptr, nullptr});
     }
-    if (bn_vec(C, ld, {dout, O, Y, dy, dres, T->p + bn_off, dgam, mean, sd})) {
+    // the gradient keeps this rank's dgamma / dbeta (summed over ranks with the rest of it);
+    // sharded, the BN backward itself needs the global sums: exchanged through xback
+    const float *ug = dgam, *ub = dbet;
+    if (T->sharded) {
+        AZ_HIP(hipMemcpyAsync(T->xback, dbet, C * sizeof(float), hipMemcpyDeviceToDevice, T->st));
+        AZ_HIP(hipMemcpyAsync(T->xback + C, dgam, C * sizeof(float), hipMemcpyDeviceToDevice, T->st));
+        TRY(exchange(T, T->xback, 2 * (size_t)C, "BatchNorm backward sums"));
+        ub = T->xback;
+        ug = T->xback + C;
+    }
+    if (bn_vec(C, ld, {dout, O, Y, dy, dres, T->p + bn_off, ug, ub, mean, sd})) {
         const unsigned g = bn_grid(C, R);
         if (bias && (size_t)g * 2 * C > T->bsum_cap) return fail("bn: bias partial buffer too small");
-        tr::bn_back4_kernel<<<g, 256, 0, T->st>>>(dout, O, Y, ld, C, R, mean, sd, T->p + bn_off, dgam, dbet, dy, dres,
-                                                  bias ? T->bsum : nullptr);
+        tr::bn_back4_kernel<<<g, 256, 0, T->st>>>(dout, O, Y, ld, C, R, mean, sd, T->p + bn_off, ug, ub, dy, dres,
+                                                  bias ? T->bsum : nullptr, nglob);
         if (bias) tr::finalize_sum_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(T->bsum, (int)g, C, bias);
     } else {
         tr::bn_back_kernel<<<grid_for((size_t)R * C), 256, 0, T->st>>>(dout, O, Y, ld, C, R, mean, sd, T->p + bn_off,
-                                                                       dgam, dbet, dy, dres);
+                                                                       ug, ub, dy, dres, nglob);
         if (bias && bias_grad(T, dy, ld, C, R, bias) != 0) return -1;
     }
     return hipGetLastError() == hipSuccess ? 0 : fail("bn backward failed");
@@ -1298,11 +1421,10 @@ int bias_grad(Trainer* T, const float* dy, int ld, int C, int R, float* dst) {
     return hipGetLastError() == hipSuccess ? 0 : fail("bias grad failed");
 }
 
-#define TRY(x) do { if ((x) != 0) return -1; } while (0)
-
 int trainer_grads(Trainer* T, const float* planes, const float* tpol, const float* tval, int B, float* losses) {
     if (B < 1 || B > T->Bmax) return fail("train: batch size out of range");
     T->last_batch = B;
+    if (T->sharded && sharded_buffers(T)) return -1;
     AZ_HIP(hipSetDevice(T->device));
     AZ_HIP(hipEventRecord(T->ev[0], T->st));
     const int F = T->F, R = B * 64;
@@ -1367,7 +1489,7 @@ int trainer_grads(Trainer* T, const float* planes, const float* tpol, const floa
     TRY(launch_conv(T, 1, T->vflat, 512, 512, T->p + L.l1w, 64, T->p + L.l1b, nullptr, T->h1, 64, B));
     // ---------------- loss + head tails
     tr::loss_kernel<<<B, 256, 0, st>>>(T->logits, T->tpol, T->h1, T->tval, T->p + L.l2w, T->p + L.l2b, B, T->dlog,
-                                       T->dh1, T->loss, T->vpart);
+                                       T->dh1, T->loss, T->vpart, T->sharded ? T->nglob : nullptr);
     {   // value_linear_2 grads: sum over boards of the per-board partials
         const int nb = nblk_rows(B);
         dim3 g(nb, 2);
@@ -1443,11 +1565,21 @@ int trainer_grads(Trainer* T, const float* planes, const float* tpol, const floa
     tr::unpack3x3_kernel<<<grid_for((size_t)9 * 19 * F), 256, 0, st>>>(T->dwtmp, F, 19, tr::X0C, T->g + L.tower[0].w);
     AZ_HIP(hipMemcpyAsync(T->hloss, T->loss, (size_t)B * 2 * sizeof(float), hipMemcpyDeviceToHost, st));
     AZ_HIP(hipStreamSynchronize(st));
+    double pl = 0.0, vl = 0.0;
+    for (int i = 0; i < B; i++) { pl += T->hloss[2 * i]; vl += T->hloss[2 * i + 1]; }
+    double nb = B;
+    if (T->sharded && (T->comm || T->host_reduce)) {   // means over the global batch
+        float h[4] = {(float)pl, (float)vl, (float)B, 0.0f};
+        AZ_HIP(hipMemcpyAsync(T->lossx, h, sizeof(h), hipMemcpyHostToDevice, st));
+        AZ_HIP(hipStreamSynchronize(st));
+        TRY(exchange(T, T->lossx, 4, "losses"));
+        AZ_HIP(hipMemcpyAsync(h, T->lossx, sizeof(h), hipMemcpyDeviceToHost, st));
+        AZ_HIP(hipStreamSynchronize(st));
+        pl = h[0]; vl = h[1]; nb = h[2];
+    }
     if (losses) {   // training.rs:281-282: means over the batch (policy, value)
-        double pl = 0.0, vl = 0.0;
-        for (int i = 0; i < B; i++) { pl += T->hloss[2 * i]; vl += T->hloss[2 * i + 1]; }
-        losses[0] = (float)(pl / B);
-        losses[1] = (float)(vl / B);
+        losses[0] = (float)(pl / nb);
+        losses[1] = (float)(vl / nb);
     }
     return 0;
 }
@@ -1485,9 +1617,14 @@ int trainer_apply(Trainer* T, double lr) {
     T->t++;
     const float bc1 = 1.0f - powi_f32(0.9f, T->t), bc2 = 1.0f - powi_f32(0.999f, T->t);
     const float decay_mul = (float)(1.0 - lr * 1e-4);   // WEIGHT_DECAY, parameters.rs:25
-    tr::adamw_kernel<<<grid_for(T->np), 256, 0, st>>>(T->p, T->g, T->m, T->v, T->mask, T->np, 1.0f / (float)T->world,
-                                                       decay_mul, (float)lr, bc1, bc2);
-    if (T->comm || T->host_reduce) {   // average the BatchNorm running statistics over ranks
+    // sharded: the summed gradient is already that of the global batch's mean loss (the loss and
+    // the BN backward normalise by the global count); per-rank batches: the mean over ranks
+    const float gscale = T->sharded ? 1.0f : 1.0f / (float)T->world;
+    tr::adamw_kernel<<<grid_for(T->np), 256, 0, st>>>(T->p, T->g, T->m, T->v, T->mask, T->np, gscale, decay_mul,
+                                                       (float)lr, bc1, bc2);
+    // average the BatchNorm running statistics over ranks (sharded: every rank already holds the
+    // same ones, updated from the global batch statistics)
+    if ((T->comm || T->host_reduce) && !T->sharded) {
         tr::stats_pack_kernel<<<grid_for(T->nstat), 256, 0, st>>>(T->p, T->stat_idx, T->nstat, T->stat_buf, 0, 1.0f);
         if (T->comm) {
             if (ncclAllReduce(T->stat_buf, T->stat_buf, T->nstat, ncclFloat, ncclSum, T->comm, st) != ncclSuccess)
@@ -1726,6 +1863,12 @@ int az_trainer_set_comm(az_trainer* t, const void* unique_id, int rank, int worl
     if (ncclCommInitRank(&T->comm, world, id, rank) != ncclSuccess) return fail("ncclCommInitRank failed");
     T->rank = rank;
     T->world = world;
+    return 0;
+}
+
+int az_trainer_set_sharded(az_trainer* t, int on) {
+    if (!t) return fail("null");
+    t->t->sharded = on != 0;
     return 0;
 }
 

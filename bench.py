@@ -80,7 +80,19 @@ def cpu_baseline(blocks, filters, threads, games, sims):
     t0 = time.perf_counter()
     steps, nsims, nevals = O.selfplay_batched(cfg, games, max_plies=1, evaluator=net.forward)
     dt = time.perf_counter() - t0
-    out = {"value": nsims / dt, "unit": "sims/s", "cores": threads, "kind": "port",
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), None)
+    except OSError:
+        pass
+    out = {"value": nsims / dt, "unit": "sims/s", "kind": "port",
+           "cores": os.cpu_count(), "nproc": len(os.sched_getaffinity(0)), "threads": threads,
+           "cores_note": "cores = os.cpu_count() of the GPU box's host, nproc = the CPUs this process may run on "
+                         "(the box's share), threads = the OpenMP / torch threads the baseline used",
+           "cpu_model": model,
+           "conv_algorithm": "oneDNN brg_conv_fwd:avx512_core, alg:convolution_direct (ONEDNN_VERBOSE=1 on the 3x3 "
+                             "and 1x1 convs of oracle/cpu_net.py: direct brgemm convolution, no Winograd)",
            "sample": "%d games x 1 move x %d sims (+ shared root eval) in lockstep, one batched f32 forward per "
                      "simulation step (torch-CPU oneDNN, BN folded), %dx%d net, %d threads, %.1f s"
                      % (games, sims, blocks, filters, threads, dt),
@@ -90,7 +102,7 @@ def cpu_baseline(blocks, filters, threads, games, sims):
     t0 = time.perf_counter()
     _, psims, _ = O.selfplay(pcfg, 16, max_plies=1)
     pdt = time.perf_counter() - t0
-    out["per_game_port"] = {"value": psims / pdt, "unit": "sims/s", "cores": threads,
+    out["per_game_port"] = {"value": psims / pdt, "unit": "sims/s", "threads": threads,
                             "sample": "16 games x 1 move x %d sims, one leaf per game at a time, naive C "
                                       "convolution (oracle/net_ref.c), %.1f s" % (max(sims // 4, 1), pdt)}
     return out
@@ -103,7 +115,7 @@ def train_child(a):
     policies, values in [-1, 1].  Prints one JSON line."""
     import numpy as np
     import azchess as A
-    rng = np.random.default_rng(1234 + a.rank)
+    rng = np.random.default_rng(1234 + (0 if a.train_mode == "sharded" else a.rank))
     B = a.train_batch
     planes = np.zeros((B, 19, 64), np.float32)
     for i in range(B):                         # piece-like one-hot planes + constant planes
@@ -118,9 +130,14 @@ def train_child(a):
         v = rng.integers(1, 40, 30).astype(np.float32)
         pol[i, idx] = v / v.sum()
     val = rng.uniform(-1, 1, B).astype(np.float32)
+    sharded = a.train_mode == "sharded"
+    if sharded:      # this rank's shard of the one global batch (the first B / world rows)
+        B //= a.world
+        planes, pol, val = planes[:B], pol[:B], val[:B]
     tr = A.Trainer(a.blocks, a.filters, max_batch=B, device=a.device, seed=42)
-    if a.world > 1:
-        tr.set_comm(bytes.fromhex(a.uid), a.rank, a.world)
+    if a.world > 1 or sharded:     # sharded at world 1: the 1-rank communicator, so its collectives are timed
+        tr.set_comm(bytes.fromhex(a.uid) if a.uid != "-" else A.comm_unique_id(), a.rank, a.world)
+    tr.set_sharded(sharded)
     for it in range(2):
         tr.step(planes, pol, val, A.get_cyclical_lr(it))
     tr.timing(reset=True)
@@ -132,18 +149,25 @@ def train_child(a):
     print(json.dumps({"ms_per_step": wall * 1e3, "device_ms_per_step": dev_ms / n, "allreduce_ms_per_step": ar_ms / n}))
 
 
-def train_phase(args, A, rank, world, local):
+def train_phase(args, A, rank, world, local, mode="per-rank"):
     """Run train_child on every rank (subprocess with a time limit, so a collective that never
-    completes cannot hold the self-play measurement hostage); rank 0 returns the summary."""
+    completes cannot hold the self-play measurement hostage); rank 0 returns the summary.
+    mode "per-rank": every rank trains its own --train-batch positions (global batch x world, per-rank
+    BatchNorm); "sharded": the reference's ONE batch of --train-batch split over the ranks, BatchNorm
+    statistics exchanged over RCCL (az_trainer_set_sharded)."""
     uid = ""
-    if world > 1:
+    sharded = mode == "sharded"
+    if world > 1 or sharded:
         import torch.distributed as dist
-        box = [A.comm_unique_id().hex() if rank == 0 else None]
-        dist.broadcast_object_list(box, src=0)
-        uid = box[0]
+        if world > 1:
+            box = [A.comm_unique_id().hex() if rank == 0 else None]
+            dist.broadcast_object_list(box, src=0)
+            uid = box[0]
+        else:
+            uid = A.comm_unique_id().hex()
     cmd = [sys.executable, os.path.abspath(__file__), "--train-child", "--rank", str(rank), "--world", str(world),
            "--device", str(local), "--uid", uid or "-", "--blocks", str(args.blocks), "--filters", str(args.filters),
-           "--train-steps", str(args.train_steps), "--train-batch", str(args.train_batch)]
+           "--train-steps", str(args.train_steps), "--train-batch", str(args.train_batch), "--train-mode", mode]
     res, err = None, None
     try:
         out = subprocess.run(cmd, capture_output=True, text=True, timeout=args.train_timeout)
@@ -163,18 +187,27 @@ def train_phase(args, A, rank, world, local):
         ms = float(t.item())
     if rank != 0:
         return None
-    flop = 3.0 * net_flop_per_eval(args.blocks, args.filters) * args.train_batch
+    gb = args.train_batch if sharded else args.train_batch * world     # global batch
+    lb = gb // world                                                    # positions per rank
+    flop = 3.0 * net_flop_per_eval(args.blocks, args.filters) * lb
     # executed MFMA work: the residual convs of forward, data grad and weight grad run as Winograd
     # F(2x2,3x3) at F = 256 (train.hip; AZ_TRAIN_WINOGRAD=0 restores direct convs)
     wino = args.filters == 256 and os.environ.get("AZ_TRAIN_WINOGRAD", "1") != "0"
-    xflop = 3.0 * executed_flop_per_eval(args.blocks, args.filters, wino) * args.train_batch
+    xflop = 3.0 * executed_flop_per_eval(args.blocks, args.filters, wino) * lb
     out = {"what": "training.rs:147-190 step: training-mode forward + backward + clip + AdamW, f32 "
                    "(v_mfma_f32_16x16x4_f32), %d positions per rank%s" %
-                   (args.train_batch, ", gradients all-reduced over RCCL" if world > 1 else ""),
-           "global_batch": args.train_batch * world, "dtype": "f32"}
+                   (lb, ", gradients all-reduced over RCCL" if world > 1 else ""),
+           "mode": mode,
+           "mode_note": ("the reference's one batch of %d split over %d rank(s); every BatchNorm's batch statistics "
+                         "and backward sums all-reduced over RCCL (2 collectives per BN per step, plus the losses "
+                         "and the gradient) -- bit-identical to the per-rank step at world 1" % (gb, world))
+                        if sharded else
+                        ("%d positions per rank, per-rank BatchNorm statistics, gradients averaged over ranks "
+                         "(global batch %d)" % (lb, gb)),
+           "global_batch": gb, "dtype": "f32"}
     if res and ms == ms and ms != float("inf"):
         tf = xflop / (res["device_ms_per_step"] * 1e-3) / 1e12
-        out.update({"ms_per_step": ms, "samples_per_s": args.train_batch * world / (ms * 1e-3),
+        out.update({"ms_per_step": ms, "samples_per_s": gb / (ms * 1e-3),
                     "device_ms_per_step": res["device_ms_per_step"],
                     "allreduce_ms_per_step": res["allreduce_ms_per_step"],
                     "allreduce_bytes": 4 * int(A._lib.lib.az_net_num_params(args.blocks, args.filters)),
@@ -385,6 +418,7 @@ def main():
     ap.add_argument("--train-steps", type=int, default=5, help="timed training steps (0 = skip the training phase)")
     ap.add_argument("--train-batch", type=int, default=512, help="positions per rank (BATCH_SIZE, parameters.rs:17)")
     ap.add_argument("--train-timeout", type=int, default=240)
+    ap.add_argument("--train-mode", default="per-rank", choices=["per-rank", "sharded"], help=argparse.SUPPRESS)
     ap.add_argument("--games-leg", type=int, default=1,
                     help="1: also play C2's games (256 x 800 sims, 6x64 f32) from startpos to the end on every rank "
                          "and report the measured games/hr (0 = skip); its wall time is in legs_wall_s")
@@ -609,6 +643,11 @@ def main():
         tl = time.perf_counter()
         training = train_phase(args, A, rank, world, local)
         legs["training"] = time.perf_counter() - tl
+        tl = time.perf_counter()
+        sh_train = train_phase(args, A, rank, world, local, mode="sharded")
+        legs["training (sharded batch)"] = time.perf_counter() - tl
+        if training is not None:
+            training["sharded_batch"] = sh_train
     if rank != 0:
         dist.destroy_process_group()
         return
@@ -672,8 +711,10 @@ def main():
         "terminal_leaf_frac": term_all / max(sims_all, 1),
         "with_fen_cache": cache_res,
         "avg_search_depth": depth_all / max(moves_all, 1),
-        "games_finished": int(fin_all),
-        "games_per_hr": fin_all / elapsed * 3600.0,
+        "games_finished_in_window": int(fin_all),
+        # the games that happen to end inside a ~1-minute window of continuous self-play are not a
+        # games/hr measurement: see games_per_hr_measured / _projected
+        "games_per_hr": None,
         "games_per_hr_measured": games_leg,
         "rank_root_digests": tot["rank_root_digests"],
         "games_per_hr_projected": None,

@@ -283,6 +283,18 @@ int az_trainer_set_comm(az_trainer* t, const void* unique_id, int rank, int worl
  * communicator set by az_trainer_set_comm. */
 typedef int (*az_allreduce_fn)(void* ctx, float* buf, size_t n);
 int az_trainer_set_host_reducer(az_trainer* t, az_allreduce_fn fn, void* ctx, int rank, int world);
+/* Sharded batch (on = 1): each rank's az_trainer_compute_grads batch is its shard of ONE global
+ * batch -- the reference's single BATCH_SIZE = 512 step (training.rs:137-159, parameters.rs:17)
+ * split over the ranks.  Every training-mode BatchNorm normalises with the statistics of the whole
+ * global batch (agent.rs:37,41,115,125,134): each BN's per-rank (sum, squared deviations, rows)
+ * are exchanged in the forward and its (sum dz, sum dz*yhat) in the backward, through the
+ * communicator or host reducer (a sum all-reduce each: 2 per BatchNorm per step, 43 BNs at
+ * 20x256); the loss and the BN backward normalise by the global row count, the summed gradient is
+ * applied unscaled, the running statistics (identical on every rank) are not averaged, and the
+ * reported losses are global means.  Off (default): each rank trains its own batch with per-rank
+ * BatchNorm statistics and the gradients are averaged (global batch = batch x world).  At one rank
+ * both modes compute the same step bit for bit. */
+int az_trainer_set_sharded(az_trainer* t, int on);
 
 /* ---- replay buffer: memory.rs ReplayBuffer, host memory ------------ */
 typedef struct az_replay az_replay;

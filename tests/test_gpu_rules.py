@@ -36,7 +36,7 @@ EXTRA_FENS = [
     "4k3/8/8/8/8/8/8/4KN2 w - - 0 1",                           # K+N vs K: insufficient
     "4kb2/8/8/8/8/8/8/2B1K3 w - - 0 1",                         # bishops on the same colour
     "4kb2/8/8/8/8/8/8/3BK3 w - - 0 1",                          # bishops on different colours
-    "8/8/8/8/8/8/1k6/K1q5 w - - 0 1",                           # white checkmated in the corner
+    "8/8/8/8/8/1k6/8/K1q5 w - - 0 1",                           # white checkmated in the corner (the kings apart: adjacent kings are refused)
     "k7/8/1Q6/8/8/8/8/K7 b - - 0 1",                            # black stalemated
     "8/8/8/3k4/3pP3/8/8/3K4 b - e3 0 1",                        # ep capture that gives no discovered check
     "8/8/8/K2pP2r/8/8/8/7k w - d6 0 1",                         # white ep illegal: horizontal pin

@@ -286,7 +286,7 @@ def test_data_parallel_world2_bit_exact(require_gpu):
     w = A.random_weights(blocks, filters, seed=21)
     planes, tpol, tval = batch(2 * n, seed=22)
     ranks = [A.Trainer(blocks, filters, weights=w, max_batch=n) for _ in range(2)]
-    slots, bar = [None, None], threading.Barrier(2)
+    slots, bar = [None, None], threading.Barrier(2, timeout=30)
 
     def reducer(rank):
         def reduce(buf):
@@ -324,3 +324,132 @@ def test_data_parallel_world2_bit_exact(require_gpu):
         assert np.array_equal(got0, got1)
         assert np.array_equal(got0, want), np.abs(got0 - want).max()
     assert not np.array_equal(gs[0], gs[1])     # the ranks saw different data
+
+
+def _run_ranks(fns):
+    """Run one callable per rank in its own thread (the ranks meet inside the host reducer);
+    re-raise the first failure."""
+    import threading
+    res, errs = [None] * len(fns), []
+
+    def run(i):
+        try:
+            res[i] = fns[i]()
+        except BaseException as e:          # noqa: B902 -- reported below
+            errs.append(e)
+    th = [threading.Thread(target=run, args=(i,), daemon=True) for i in range(len(fns))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not any(t.is_alive() for t in th), "a rank hung"
+    if errs:
+        raise errs[0]
+    return res
+
+
+def _host_reducer_pair():
+    import threading
+    slots, bar = [None, None], threading.Barrier(2, timeout=60)
+
+    def reducer(rank):
+        def reduce(buf):
+            slots[rank] = buf.copy()
+            bar.wait()
+            buf[:] = slots[0] + slots[1]
+            bar.wait()
+        return reduce
+    return reducer
+
+
+@pytest.mark.parametrize("blocks,filters", [(2, 64), (2, 256)])
+def test_sharded_world1_rccl_is_the_plain_step(require_gpu, blocks, filters):
+    """az_trainer_set_sharded over a 1-rank RCCL communicator: every BatchNorm's statistics and
+    backward sums, the losses and the gradients go through ncclAllReduce, and the step is the
+    plain step bit for bit (F = 64: column-sum statistics; F = 256: the Winograd epilogues'
+    per-board statistics)."""
+    w = A.random_weights(blocks, filters, seed=31)
+    planes, tpol, tval = batch(16, seed=32)
+    a = A.Trainer(blocks, filters, weights=w, max_batch=16)
+    b = A.Trainer(blocks, filters, weights=w, max_batch=16)
+    b.set_comm(A.comm_unique_id(), 0, 1)
+    b.set_sharded(True)
+    for it in range(2):
+        la = a.compute_gradients(planes, tpol, tval)
+        lb = b.compute_gradients(planes, tpol, tval)
+        assert np.allclose(la, lb, rtol=1e-6, atol=0), (la, lb)
+        assert np.array_equal(a.grads(), b.grads())
+        assert np.array_equal(a.params(), b.params())
+        a.apply(A.get_cyclical_lr(it))
+        b.apply(A.get_cyclical_lr(it))
+        assert np.array_equal(a.params(), b.params())
+
+
+def test_sharded_world2_host_reducer_matches_single_batch(require_gpu):
+    """the reference trains ONE batch of 512 (training.rs:137-159,
+    parameters.rs:17) with batch-512 BatchNorm statistics (agent.rs:37,41,115).  Two ranks in
+    sharded mode (az_trainer_set_sharded, exchanges through the host reducer), 256 positions each,
+    against one rank on all 512, both against the float64 oracle on the 512-position batch under
+    each path's own ReLU masks (the two ranks' masks concatenated):
+      losses (global means)            |d| <= 1e-5 (1 + |ref|), and against the 1-rank step
+      every gradient tensor            <= 1e-4 relative norm vs the oracle (sharded: g0 + g1)
+      sharded vs 1-rank, per tensor    <= 1e-2 relative norm (different ReLU branches near 0)
+      running statistics               <= 1e-5 vs the oracle; bit-identical on the two ranks
+    then the AdamW step: both ranks bit-identical and equal to T.adamw_step(p, g0 + g1, world=1)."""
+    blocks, filters, n = 2, 256, 512
+    h = n // 2
+    w = A.random_weights(blocks, filters, seed=41)
+    planes, tpol, tval = batch(n, seed=42)
+    one = A.Trainer(blocks, filters, weights=w, max_batch=n)
+    l1 = one.compute_gradients(planes, tpol, tval)
+    g1, p1, m1 = one.grads(), one.params(), one.relu_masks(n)
+    ranks = [A.Trainer(blocks, filters, weights=w, max_batch=h) for _ in range(2)]
+    red = _host_reducer_pair()
+    for r, tr in enumerate(ranks):
+        tr.set_host_reducer(red(r), r, 2)
+        tr.set_sharded(True)
+    ls = _run_ranks([lambda r=r, tr=tr: tr.compute_gradients(planes[r * h:(r + 1) * h], tpol[r * h:(r + 1) * h],
+                                                             tval[r * h:(r + 1) * h]) for r, tr in enumerate(ranks)])
+    assert ls[0] == ls[1]                     # global means on both ranks
+    gs = [tr.grads() for tr in ranks]
+    ps = [tr.params() for tr in ranks]
+    ms = [tr.relu_masks(h) for tr in ranks]
+    msh = [np.concatenate([a, b]) for a, b in zip(ms[0], ms[1])]
+    gsh = gs[0].astype(np.float64) + gs[1].astype(np.float64)
+    stats = ~T.trainable_mask(blocks, filters)
+    assert np.array_equal(ps[0][stats], ps[1][stats])
+    seg, _ = T.segments(blocks, filters)
+    zero_bias = bn_fed_biases(blocks)
+    for name_path, (loss, g, p, masks) in {"1-rank": (l1, g1, p1, m1), "sharded": (ls[0], gsh, ps[0], msh)}.items():
+        ref = T.TrainRef(blocks, filters, w)
+        rg, (rpl, rvl) = ref.grads(planes, tpol, tval, masks)
+        assert abs(loss[0] - rpl) <= 1e-5 * (1 + abs(rpl)) and abs(loss[1] - rvl) <= 1e-5 * (1 + abs(rvl)), \
+            (name_path, loss, rpl, rvl)
+        rs = ref.running_stats_flat(w)
+        assert np.all(np.abs(p[stats] - rs[stats]) <= 1e-5 * (1 + np.abs(rs[stats]))), name_path
+        for name, (o, shape, bn) in seg.items():
+            parts = [(name + ".gamma", o, shape[1]), (name + ".beta", o + shape[1], shape[1])] if bn else \
+                [(name, o, int(np.prod(shape)))]
+            for pname, off, cnt in parts:
+                a = np.asarray(g[off:off + cnt], np.float64)
+                if pname in zero_bias:
+                    assert np.abs(a).max() <= 1e-5, (name_path, pname)
+                    continue
+                r = rg[off:off + cnt]
+                err = np.linalg.norm(a - r) / max(np.linalg.norm(r), 1e-30)
+                assert err <= 1e-4, (name_path, pname, err)
+    assert abs(ls[0][0] - l1[0]) <= 1e-5 * (1 + abs(l1[0])) and abs(ls[0][1] - l1[1]) <= 1e-5 * (1 + abs(l1[1]))
+    for name, (o, shape, bn) in seg.items():
+        if name in zero_bias:
+            continue
+        cnt = 2 * shape[1] if bn else int(np.prod(shape))
+        r = g1[o:o + cnt].astype(np.float64)
+        assert np.linalg.norm(gsh[o:o + cnt] - r) <= 1e-2 * max(np.linalg.norm(r), 1e-30), name
+    # the optimizer step: gradients summed by the reducer, applied unscaled (global-mean loss)
+    lr = A.get_cyclical_lr(4)
+    _run_ranks([lambda tr=tr: tr.apply(lr) for tr in ranks])
+    mask = T.trainable_mask(blocks, filters)
+    want, _, _ = T.adamw_step(ps[0], gs[0] + gs[1], np.zeros_like(w), np.zeros_like(w), mask, 1, lr, world=1)
+    got0, got1 = ranks[0].params(), ranks[1].params()
+    assert np.array_equal(got0, got1)
+    assert np.array_equal(got0, want), np.abs(got0 - want).max()

@@ -6,6 +6,7 @@ import numpy as np
 import pytest
 
 import azchess as A
+from azchess import _lib as L
 import oracle as O
 
 EDGE_FENS = [
@@ -76,3 +77,46 @@ def test_illegal_index_rejected():
     assert A.index_to_move(0, p) is None        # a1 has a rook that cannot jump
     with pytest.raises(A.IllegalMove):
         A.play_move(A.GameState(), 0)
+
+
+# setups shakmaty's Chess::from_setup refuses: the engine sizes a node's edges for
+# 218 legal moves, so a root or probe parent outside them must be refused on the host
+BAD_FENS = [
+    "QQQQQQQQ/QQQQQQQQ/8/8/8/8/8/K6k w - - 0 1",          # too much material (many queens)
+    "Q7/QQ6/1Q6/2Q5/3Q4/4Q3/5Q2/K5Qk w - - 0 1",          # 10 queens, no pawns: promoted excess
+    "4k3/8/8/8/8/8/PPPPPPPP/P3K3 w - - 0 1",             # 9 pawns, one on the back rank
+    "4k3/8/8/8/8/8/8/P3K3 w - - 0 1",                    # pawn on the first rank
+    "4k3/8/8/8/8/8/4R3/4K3 w - - 0 1",                   # side not to move in check
+    "4k3/8/8/8/8/8/8/4K3 w - e6 0 1",                    # ep square without the pushed pawn... (dropped: no capturer)
+    "4k3/8/8/3P4/8/8/8/4K3 w - e6 0 1",                   # ep square a pawn could take, no pushed pawn
+    "8/8/8/8/8/8/8/8 w - - 0 1",                         # no kings
+    "k7/8/8/8/8/8/8/KK6 w - - 0 1",                      # two white kings
+    "4k3/8/8/8/8/5n2/3b4/r3K3 w - - 0 1",                # triple check
+]
+
+
+@pytest.mark.parametrize("fen", [f for i, f in enumerate(BAD_FENS) if i != 5])
+def test_invalid_setups_refused(fen):
+    with pytest.raises(L.AzError):
+        A.Position.from_fen(fen)
+
+
+def test_ep_without_capturer_is_dropped_not_refused():
+    # shakmaty keeps only a pseudo-legal ep square; one no pawn can take is simply absent
+    assert A.Position.from_fen(BAD_FENS[5]).fen() == "4k3/8/8/8/8/8/8/4K3 w - - 0 1"
+
+
+def test_probe_refuses_bad_parent_before_any_device_call():
+    """az_rules_probe validates every parent on the host (its device scratch holds MAX_EDGES
+    moves); the refusal comes before hipSetDevice, so this runs without a GPU."""
+    from azchess.chess import positions_to_array, rules_probe
+    good = positions_to_array([A.Position.from_fen("4k3/8/8/8/8/8/8/4K2R w K - 0 1")])
+    bad = good.copy()
+    bad["castling"] = 2                    # white O-O-O right with no rook on a1
+    with pytest.raises(L.AzError, match="castling"):
+        rules_probe(bad, [-1])
+    queens = good.copy()
+    queens["bb"][0, 4] |= 0x00FFFF0000000000   # 16 extra white queens
+    queens["bb"][0, 6] |= 0x00FFFF0000000000
+    with pytest.raises(L.AzError, match="material"):
+        rules_probe(queens, [-1])
