@@ -194,7 +194,7 @@ SEARCH_ROOTS = [
     ("3k4/8/8/8/8/8/8/3KQ3 b - - 0 199", []),                    # 200-fullmove draw one ply down
     ("r3k2r/p1ppqpb1/bn2pnp1/3PN3/1p2P3/2N2Q1p/PPPBBPPP/R3K2R w KQkq - 0 1", []),
     ("R6R/3Q4/1Q4Q1/4Q3/2Q4Q/Q4Q2/pp1Q4/kBNN1KB1 w - - 0 1", []),   # 218 edges: select's > 64 path
-    ("7k/8/6K1/8/8/8/8/Q7 w - - 0 1", []),                       # mate in one
+    ("7k/8/6K1/8/8/8/Q7/8 w - - 0 1", []),                       # mate in one (Qa8#)
 ]
 
 

@@ -83,7 +83,7 @@ def test_illegal_index_rejected():
 # 218 legal moves, so a root or probe parent outside them must be refused on the host
 BAD_FENS = [
     "QQQQQQQQ/QQQQQQQQ/8/8/8/8/8/K6k w - - 0 1",          # too much material (many queens)
-    "Q7/QQ6/1Q6/2Q5/3Q4/4Q3/5Q2/K5Qk w - - 0 1",          # 10 queens, no pawns: promoted excess
+    "k7/8/8/8/8/8/3QQQQQ/2QQQQQK w - - 0 1",              # 10 queens, no pawns: promoted excess
     "4k3/8/8/8/8/8/PPPPPPPP/P3K3 w - - 0 1",             # 9 pawns, one on the back rank
     "4k3/8/8/8/8/8/8/P3K3 w - - 0 1",                    # pawn on the first rank
     "4k3/8/8/8/8/8/4R3/4K3 w - - 0 1",                   # side not to move in check
