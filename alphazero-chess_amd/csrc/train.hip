@@ -515,6 +515,16 @@ __global__ void finalize_sum_kernel(const float* __restrict__ part, int nblk, in
     if (lane == 0) dst[c] = s;
 }
 
+// the bias gradients of every BN-fed conv of the step in one launch (they are needed only by the
+// optimizer): blockIdx.y = BatchNorm j, its bn_back4 partials at part + j pstride, its gradient at
+// g + dst[j]
+__global__ void finalize_sum_batched_kernel(const float* __restrict__ part, size_t pstride, int nblk, int C,
+                                            const uint32_t* __restrict__ dst, float* __restrict__ g) {
+    FIN_CHANNEL();
+    const float s = part_sum(part + blockIdx.y * pstride, nblk, C, c, 0, lane);
+    if (lane == 0) g[dst[blockIdx.y] + c] = s;
+}
+
 // mean[c] = sum / R
 __global__ void finalize_mean_kernel(const float* __restrict__ part, int nblk, int C, int R, float* __restrict__ mean) {
     FIN_CHANNEL();
@@ -870,6 +880,24 @@ struct BoardStats {
     const float* mean;   // STATS 2
     const float* stdv;   // STATS 2
 };
+// BNIN: the conv's input is the BatchNorm + ReLU (+ residual) of the previous conv's output,
+// applied while the board's rows are staged (bn_apply4_kernel's arithmetic, element for element),
+// and written out as the saved activation the backward needs -- the separate bn_apply pass over
+// the 32 MB layer (a read of Y and the residual, a write, and the conv's re-read) is gone.
+struct BnIn {
+    const float *mean, *stdv, *gamma, *beta;
+    const float* res;    // the block input added before the ReLU (BN2), or null (BN0 / BN1)
+    float* out;          // relu(bn(X) [+ res]): hh[b] or xs[b]
+};
+// XIN 2 (data-grad convs): the conv's input dy is the BatchNorm backward of X = dout (the ReLU
+// output's gradient), computed while the board's rows are staged (bn_back4_kernel's arithmetic,
+// element for element) and written out for the weight grad; dres (BN2) gets dz; bsum gets the
+// board's sum of dy per channel (the producing conv's bias gradient, summed over boards later)
+struct BnBack {
+    const float *O, *Y, *mean, *stdv, *gamma, *dgamma, *dbeta, *nglob;
+    float *dy, *dres, *bsum;
+    int R;
+};
 __device__ __forceinline__ f32x4 sum16(f32x4 v) {   // over the 16 lanes of a row (fixed butterfly)
 #pragma unroll
     for (int m = 1; m < 16; m <<= 1)
@@ -877,11 +905,11 @@ __device__ __forceinline__ f32x4 sum16(f32x4 v) {   // over the 16 lanes of a ro
         for (int r = 0; r < 4; r++) v[r] += __shfl_xor(v[r], m, 64);
     return v;
 }
-template <bool ADD, int STATS>
+template <bool ADD, int STATS, int XIN>
 __global__ void __launch_bounds__(512)
 conv_wino_train_kernel(const float* __restrict__ X, const uint4* __restrict__ U, unsigned ubytes,
                        const float* __restrict__ bias, const float* __restrict__ addend, float* __restrict__ Y,
-                       BoardStats bs) {
+                       BoardStats bs, BnIn bn, BnBack bb) {
     constexpr int F = 256, NN = WinoCfg<F>::NN, XSn = WinoCfg<F>::XS, PF = WinoCfg<F>::PF, RS = F / 4 + 2;
     constexpr int XSZ = 64 * RS, VSZ = 2 * WinoCfg<F>::CH * 1024 / 16, PAD = WINO_PAD_SQ * RS;
     __shared__ __attribute__((aligned(16))) uint4 lds[PAD + XSZ + PAD + VSZ];
@@ -889,12 +917,73 @@ conv_wino_train_kernel(const float* __restrict__ X, const uint4* __restrict__ U,
     const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const size_t row0 = (size_t)vgpr_index(blockIdx.x) * 64;
     const uint4* X4 = reinterpret_cast<const uint4*>(X) + row0 * (F / 4);
-    for (int c = tid; c < 64 * (F / 4); c += 512) act[(c / (F / 4)) * RS + c % (F / 4)] = X4[c];
+    if constexpr (XIN == 1) {   // thread = channel quad tid % 64 (F / 4 = 64 divides 512) x rows tid / 64 + 8 k
+        static_assert(F / 4 == 64, "BNIN staging assumes 64 channel quads");
+        const int cq = tid & 63;
+        const float4 mu = reinterpret_cast<const float4*>(bn.mean)[cq], sd = reinterpret_cast<const float4*>(bn.stdv)[cq];
+        const float4 ga = reinterpret_cast<const float4*>(bn.gamma)[cq], be = reinterpret_cast<const float4*>(bn.beta)[cq];
+        const float4* R4 = bn.res ? reinterpret_cast<const float4*>(bn.res) + row0 * (F / 4) : nullptr;
+        float4* O4 = reinterpret_cast<float4*>(bn.out) + row0 * (F / 4);
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const int c = tid + 512 * k;
+            const float4 y = reinterpret_cast<const float4*>(X4)[c];
+            float4 v = make_float4(((y.x - mu.x) / sd.x) * ga.x + be.x, ((y.y - mu.y) / sd.y) * ga.y + be.y,
+                                   ((y.z - mu.z) / sd.z) * ga.z + be.z, ((y.w - mu.w) / sd.w) * ga.w + be.w);
+            if (R4) {
+                const float4 q = R4[c];
+                v.x += q.x; v.y += q.y; v.z += q.z; v.w += q.w;
+            }
+            const float4 o = make_float4(fmaxf(v.x, 0.0f), fmaxf(v.y, 0.0f), fmaxf(v.z, 0.0f), fmaxf(v.w, 0.0f));
+            O4[c] = o;
+            act[(c / (F / 4)) * RS + cq] = __builtin_bit_cast(uint4, o);
+        }
+    } else if constexpr (XIN == 2) {   // the same thread layout; X = dout
+        static_assert(F / 4 == 64, "BnBack staging assumes 64 channel quads");
+        const int cq = tid & 63;
+        const float invR = 1.0f / (bb.nglob ? *bb.nglob : (float)bb.R);
+        const float4 mu = reinterpret_cast<const float4*>(bb.mean)[cq], sd = reinterpret_cast<const float4*>(bb.stdv)[cq];
+        const float4 ga = reinterpret_cast<const float4*>(bb.gamma)[cq], dg = reinterpret_cast<const float4*>(bb.dgamma)[cq];
+        const float4 db = reinterpret_cast<const float4*>(bb.dbeta)[cq];
+        const size_t o0 = row0 * (F / 4);
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const size_t c = o0 + tid + 512 * k;
+            const float4 d = reinterpret_cast<const float4*>(X)[c], ov = reinterpret_cast<const float4*>(bb.O)[c];
+            const float4 y = reinterpret_cast<const float4*>(bb.Y)[c];
+            const float4 dz = make_float4(ov.x > 0.0f ? d.x : 0.0f, ov.y > 0.0f ? d.y : 0.0f, ov.z > 0.0f ? d.z : 0.0f,
+                                          ov.w > 0.0f ? d.w : 0.0f);
+            const float4 d4 = make_float4((ga.x / sd.x) * (dz.x - db.x * invR - ((y.x - mu.x) / sd.x) * dg.x * invR),
+                                          (ga.y / sd.y) * (dz.y - db.y * invR - ((y.y - mu.y) / sd.y) * dg.y * invR),
+                                          (ga.z / sd.z) * (dz.z - db.z * invR - ((y.z - mu.z) / sd.z) * dg.z * invR),
+                                          (ga.w / sd.w) * (dz.w - db.w * invR - ((y.w - mu.w) / sd.w) * dg.w * invR));
+            reinterpret_cast<float4*>(bb.dy)[c] = d4;
+            if (bb.dres) reinterpret_cast<float4*>(bb.dres)[c] = dz;
+            act[(tid + 512 * k) / (F / 4) * RS + cq] = __builtin_bit_cast(uint4, d4);
+            acc.x += d4.x; acc.y += d4.y; acc.z += d4.z; acc.w += d4.w;
+        }
+        // the board's bias partial: the 8 row phases of each channel quad, in order, through the
+        // (not yet written) V buffers
+        float4* red = reinterpret_cast<float4*>(lds + PAD + XSZ + PAD);
+        red[tid] = acc;
+        __syncthreads();
+        if (tid < 64) {
+            float4 a = red[tid];
+            for (int k = 1; k < 8; k++) {
+                const float4 q = red[64 * k + tid];
+                a.x += q.x; a.y += q.y; a.z += q.z; a.w += q.w;
+            }
+            reinterpret_cast<float4*>(bb.bsum + (size_t)vgpr_index(blockIdx.x) * 2 * F)[tid] = a;   // [board][2][F]
+        }
+    } else {
+        for (int c = tid; c < 64 * (F / 4); c += 512) act[(c / (F / 4)) * RS + c % (F / 4)] = X4[c];
+    }
     for (int c = tid; c < PAD; c += 512) {
         lds[c] = make_uint4(0, 0, 0, 0);
         act[XSZ + c] = make_uint4(0, 0, 0, 0);
     }
-    __syncthreads();
+    __syncthreads();   // (XIN 2: also orders the bias partial's reads of V before wino_core writes V)
     const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc((void*)U, (short)0, (int)ubytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rN = __builtin_amdgcn_make_buffer_rsrc((void*)U, (short)0, 0, 0x00020000);
     const int voff = wino_voff<F>(w, lane);
@@ -1015,17 +1104,26 @@ __global__ void repack3x3_kernel(const float* __restrict__ w, int co_n, int ci_n
 // The split reduction and dW = G^T dU G in one pass: dU[xi][e] = sum over splits s (in order) of
 // partial[s][xi][e], e = ci F + co, then dW[co][ci] = G^T dU G in f64, rounded once, into the
 // gradient's burn layout g[co][ci][3][3] (bit-identical to the round-3 reduce_kernel + separate
-// transform, 13.4 + 5.7 us per conv, without the dU round trip).  Workgroup = 64 e (lanes) x 16
-// waves, wave = point xi: each thread's 16 split loads are independent (4 points per wave
-// measured 23.2 us: too few loads in flight), the points meet in LDS, waves 0-2 write kernel row ky.
-__global__ void __launch_bounds__(1024) wino_wgrad_reduce_out_kernel(const float* __restrict__ partial, int splits,
-                                                                     int F, float* __restrict__ g) {
+// transform, 13.4 + 5.7 us per conv, without the dU round trip).  Workgroup = 64 e (lanes) x NW
+// waves, wave w = points w, w + NW, ...: each thread's split loads per point are independent (16
+// waves of one point: 15.5 us alone; 4 points per wave measured 23.2 us: too few loads in flight),
+// the points meet in LDS, waves 0-2 write kernel row ky.  (Round 5: NW = 4 -- 256 threads, which
+// fit beside a Winograd conv workgroup on its CU -- on a second stream beside the next data-grad
+// conv measured slower than in sequence, 22.72 vs 22.20 ms per step, as did the whole weight grad
+// on a second stream (22.67 vs 22.62): its 256-VGPR workgroups hold their CUs for the whole GEMM,
+// so the data-grad chain's small kernels queued behind them.  Not kept.)
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) wino_wgrad_reduce_out_kernel(const float* __restrict__ partial, int splits,
+                                                                        int F, float* __restrict__ g) {
     __shared__ float su[16][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const size_t n = (size_t)F * F, e = (size_t)blockIdx.x * 64 + lane;
-    float s = 0.0f;
-    for (int k = 0; k < splits; k++) s += partial[((size_t)k * 16 + w) * n + e];
-    su[w][lane] = s;
+#pragma unroll
+    for (int xi = w; xi < 16; xi += NW) {
+        float s = 0.0f;
+        for (int k = 0; k < splits; k++) s += partial[((size_t)k * 16 + xi) * n + e];
+        su[xi][lane] = s;
+    }
     __syncthreads();
     if (w >= 3) return;
     const int ky = w, co = (int)(e % F), ci = (int)(e / F);
@@ -1178,6 +1276,13 @@ struct Trainer {
     bool sharded = false;
     float *xfwd = nullptr, *xback = nullptr, *nglob = nullptr, *lossx = nullptr;
     int xfwd_world = 0;
+    bool fuse_bn = true;                     // BN apply / backward staged in the next Winograd conv (env AZ_TRAIN_FUSE_BN=0: off)
+    // the conv bias gradients of the tower's BatchNorms: bn_back4 partials per BN, summed in one
+    // launch at the end of the backward (bias_dst[j] = gradient offset of BN j's conv bias)
+    float* bsum_all = nullptr;
+    size_t bsum_stride = 0;
+    uint32_t* bias_dst = nullptr;
+    std::vector<int> bias_pending;           // per BN: 0, or the partial blocks to sum
     std::vector<void*> allocs;
     // timing (HIP events on the trainer stream): whole steps and the gradient all-reduce
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -1214,21 +1319,32 @@ int launch_conv(Trainer* T, int taps, const float* X, int ldx, int K, const floa
 
 // Y = conv3x3(X, U) (+ bias) (+ addend) over B whole boards, Winograd (F = 256 residual convs);
 // stats 1 / 2: per-board BN partials into bs.part (tr::BoardStats)
+// bn.out non-null: X is the previous conv's pre-BN output, BatchNorm + ReLU (+ bn.res) applied in
+// the staging and written to bn.out (tr::BnIn)
+// bb.dy non-null: X is the BN backward's dout, the backward staged (tr::BnBack)
 int launch_wino(Trainer* T, const float* X, const float* U, const float* bias, const float* addend, float* Y, int B,
-                int stats = 0, tr::BoardStats bs = {}) {
+                int stats = 0, tr::BoardStats bs = {}, tr::BnIn bn = {}, tr::BnBack bb = {}) {
     const uint4* U4 = reinterpret_cast<const uint4*>(U);
     const unsigned ub = (unsigned)T->ubytes;
     if (stats && !bs.part) return fail("Winograd conv: statistics without a buffer");
-    if (addend && stats == 2)
-        tr::conv_wino_train_kernel<true, 2><<<B, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs);
+    if (bn.out && (addend || stats != 1)) return fail("Winograd conv: BatchNorm staging is a forward conv's");
+    if (bb.dy && stats != 2) return fail("Winograd conv: the BN backward staging is a data-grad conv's");
+    if (bn.out)
+        tr::conv_wino_train_kernel<false, 1, 1><<<B, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb);
+    else if (bb.dy && addend)
+        tr::conv_wino_train_kernel<true, 2, 2><<<B, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb);
+    else if (bb.dy)
+        tr::conv_wino_train_kernel<false, 2, 2><<<B, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb);
+    else if (addend && stats == 2)
+        tr::conv_wino_train_kernel<true, 2, 0><<<B, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb);
     else if (addend && stats == 0)
-        tr::conv_wino_train_kernel<true, 0><<<B, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs);
+        tr::conv_wino_train_kernel<true, 0, 0><<<B, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb);
     else if (!addend && stats == 1)
-        tr::conv_wino_train_kernel<false, 1><<<B, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs);
+        tr::conv_wino_train_kernel<false, 1, 0><<<B, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb);
     else if (!addend && stats == 2)
-        tr::conv_wino_train_kernel<false, 2><<<B, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs);
+        tr::conv_wino_train_kernel<false, 2, 0><<<B, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb);
     else if (!addend && stats == 0)
-        tr::conv_wino_train_kernel<false, 0><<<B, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs);
+        tr::conv_wino_train_kernel<false, 0, 0><<<B, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb);
     else
         return fail("Winograd conv: unsupported statistics mode");
     return hipGetLastError() == hipSuccess ? 0 : fail("Winograd conv launch failed");
@@ -1270,10 +1386,10 @@ int launch_wino_wgrad(Trainer* T, const float* X, const float* DY, int B, float*
     const int splits = (int)wino_gemm_splits(B);
     if (splits * 16 * (size_t)F * F > T->wpart_cap) return fail("Winograd wgrad: partial buffer too small");
     if ((size_t)B * 64 * F * 4 >= (size_t)0x40000000) return fail("Winograd wgrad: batch too large for 32-bit offsets");
-    hipStream_t st = T->st;
-    tr::wino_wgrad_gemm_kernel<<<dim3(splits, 16), 512, 0, st>>>(X, DY, K, WINO_GEMM_ROWS, T->wpart);
     if ((size_t)F * F % 64) return fail("Winograd wgrad: F * F must be a multiple of 64");
-    tr::wino_wgrad_reduce_out_kernel<<<(unsigned)((size_t)F * F / 64), 1024, 0, st>>>(T->wpart, splits, F, g);
+    const unsigned rblocks = (unsigned)((size_t)F * F / 64);
+    tr::wino_wgrad_gemm_kernel<<<dim3(splits, 16), 512, 0, T->st>>>(X, DY, K, WINO_GEMM_ROWS, T->wpart);
+    tr::wino_wgrad_reduce_out_kernel<16><<<rblocks, 1024, 0, T->st>>>(T->wpart, splits, F, g);
     return hipGetLastError() == hipSuccess ? 0 : fail("Winograd wgrad launch failed");
 }
 
@@ -1296,13 +1412,15 @@ int exchange(Trainer* T, float* d, size_t n, const char* what) {
 // sharded batch: the exchange buffers for the current world (allocated on first use)
 int sharded_buffers(Trainer* T) {
     if (T->xfwd && T->xfwd_world == T->world) return 0;
-    const size_t n = (size_t)T->world * (2 * T->slot + 1) + 2 * (size_t)T->slot + 8;
-    float* q = T->alloc(n);
+    // every piece 256-byte aligned: the BN backward takes its four-channel path on the exchanged
+    // sums exactly when it does on the rank's own (bn_vec), so one rank computes the plain step
+    const size_t nf = ((size_t)T->world * (2 * T->slot + 1) + 63) & ~(size_t)63, nb = ((size_t)2 * T->slot + 63) & ~(size_t)63;
+    float* q = T->alloc(nf + nb + 128);
     if (!q) return fail("sharded batch: out of device memory");
     T->xfwd = q;
-    T->xback = q + (size_t)T->world * (2 * T->slot + 1);
-    T->nglob = T->xback + 2 * T->slot;
-    T->lossx = T->nglob + 4;
+    T->xback = q + nf;
+    T->nglob = T->xback + nb;
+    T->lossx = T->nglob + 64;
     T->xfwd_world = T->world;
     return 0;
 }
@@ -1324,6 +1442,7 @@ unsigned bn_grid(int C, int R) {
 // BatchNorm (training) + ReLU (+ residual): Y -> out; saves mean/std in slot `bi`
 // bpart: per-board partials from the producing conv's epilogue (tr::BoardStats, STATS 1) instead
 // of the two column-sum passes
+// out == nullptr: the statistics only (the apply is staged in the next Winograd conv, tr::BnIn)
 int bn_forward(Trainer* T, int bi, const float* Y, int ld, int C, int R, size_t bn_off, const float* res, float* out,
                const float* bpart = nullptr) {
     float* P = T->p + bn_off;   // {gamma, beta, running_mean, running_var}
@@ -1362,6 +1481,7 @@ int bn_forward(Trainer* T, int bi, const float* Y, int ld, int C, int R, size_t 
         tr::launch_colsum<1>(g, T->st, Y, ld, C, R, mean, nullptr, nullptr, nullptr, T->cpart,
                              {tr::FIN_VAR, sd, P + 2 * C, P + 3 * C, mean});
     }
+    if (!out) return hipGetLastError() == hipSuccess ? 0 : fail("bn statistics failed");
     if (bn_vec(C, ld, {Y, res, out, P, mean, sd}))
         tr::bn_apply4_kernel<<<bn_grid(C, R), 256, 0, T->st>>>(Y, ld, C, R, mean, sd, P, P + C, res, out);
     else
@@ -1369,17 +1489,25 @@ int bn_forward(Trainer* T, int bi, const float* Y, int ld, int C, int R, size_t 
     return hipGetLastError() == hipSuccess ? 0 : fail("bn forward failed");
 }
 
+// BatchNorm bi applied in the next Winograd conv's staging (statistics from bn_forward(out = null))
+tr::BnIn bn_in(Trainer* T, int bi, size_t bn_off, const float* res, float* out) {
+    const float* P = T->p + bn_off;
+    return tr::BnIn{T->bmean + (size_t)bi * T->slot, T->bstd + (size_t)bi * T->slot, P, P + T->F, res, out};
+}
+
 // BN backward: dout (grad of the ReLU output O), pre-BN Y -> dy; dgamma/dbeta into the grad buffer
 // bpart: per-board dz / dz*yhat sums from the conv that produced dout (tr::BoardStats, STATS 2)
 // bias: the producing conv's bias gradient (sum of dy over rows), fused into the BN backward
 int bias_grad(Trainer* T, const float* dy, int ld, int C, int R, float* dst);
-int bn_backward(Trainer* T, int bi, const float* dout, const float* O, const float* Y, int ld, int C, int R,
-                size_t bn_off, float* dy, float* dres, const float* bpart = nullptr, float* bias = nullptr) {
+// the BN backward's sums: dgamma / dbeta of this rank into the gradient (from the producing conv's
+// per-board partials, or column sums), then -- sharded -- their global sums through xback;
+// *ug / *ub: the sums the backward itself uses
+int bn_back_sums(Trainer* T, int bi, const float* dout, const float* O, const float* Y, int ld, int C, int R,
+                 size_t bn_off, const float* bpart, const float** ug_out, const float** ub_out) {
     const float* mean = T->bmean + (size_t)bi * T->slot;
     const float* sd = T->bstd + (size_t)bi * T->slot;
     float* dgam = T->g + bn_off;
     float* dbet = T->g + bn_off + C;
-    const float* nglob = T->sharded ? T->nglob : nullptr;
     if (bpart) {
         if (R % 64 || ld != C) return fail("bn: board statistics need whole boards");
         tr::finalize_bnback_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(bpart, R / 64, C, dgam, dbet);
@@ -1399,12 +1527,44 @@ int bn_backward(Trainer* T, int bi, const float* dout, const float* O, const flo
         ub = T->xback;
         ug = T->xback + C;
     }
-    if (bn_vec(C, ld, {dout, O, Y, dy, dres, T->p + bn_off, ug, ub, mean, sd})) {
+    *ug_out = ug;
+    *ub_out = ub;
+    return hipGetLastError() == hipSuccess ? 0 : fail("bn backward sums failed");
+}
+
+// the BN backward of BN bi staged in the next Winograd data-grad conv (tr::BnBack): its sums here,
+// the element-wise part in the conv's staging; bias partials per board, summed at the end
+int bn_back_fused(Trainer* T, int bi, const float* dout, const float* O, const float* Y, int R, size_t bn_off,
+                  const float* bpart, float* dy, float* dres, tr::BnBack* bb) {
+    const int C = T->F, B = R / 64;
+    const float *ug, *ub;
+    TRY(bn_back_sums(T, bi, dout, O, Y, C, C, R, bn_off, bpart, &ug, &ub));
+    if ((size_t)B * 2 * C > T->bsum_stride || bi >= (int)T->bias_pending.size()) return fail("bn: fused backward: bad shape");
+    *bb = tr::BnBack{O, Y, T->bmean + (size_t)bi * T->slot, T->bstd + (size_t)bi * T->slot, T->p + bn_off, ug, ub,
+                     T->sharded ? T->nglob : nullptr, dy, dres, T->bsum_all + (size_t)bi * T->bsum_stride, R};
+    T->bias_pending[bi] = B;     // partials per board
+    return 0;
+}
+
+int bn_backward(Trainer* T, int bi, const float* dout, const float* O, const float* Y, int ld, int C, int R,
+                size_t bn_off, float* dy, float* dres, const float* bpart = nullptr, float* bias = nullptr) {
+    const float* mean = T->bmean + (size_t)bi * T->slot;
+    const float* sd = T->bstd + (size_t)bi * T->slot;
+    float* dgam = T->g + bn_off;
+    float* dbet = T->g + bn_off + C;
+    const float* nglob = T->sharded ? T->nglob : nullptr;
+    const float *ug, *ub;
+    TRY(bn_back_sums(T, bi, dout, O, Y, ld, C, R, bn_off, bpart, &ug, &ub));
+    if (bn_vec(C, ld, {dout, O, Y, dy, dres, T->p + bn_off, dgam, dbet, ug, ub, mean, sd})) {
         const unsigned g = bn_grid(C, R);
         if (bias && (size_t)g * 2 * C > T->bsum_cap) return fail("bn: bias partial buffer too small");
+        // the tower's conv biases: partials kept per BN, summed at the end of the backward in one launch
+        const bool batched = bias && T->bsum_all && bi < (int)T->bias_pending.size() && C == T->F;
+        float* bs = batched ? T->bsum_all + (size_t)bi * T->bsum_stride : T->bsum;
         tr::bn_back4_kernel<<<g, 256, 0, T->st>>>(dout, O, Y, ld, C, R, mean, sd, T->p + bn_off, ug, ub, dy, dres,
-                                                  bias ? T->bsum : nullptr, nglob);
-        if (bias) tr::finalize_sum_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(T->bsum, (int)g, C, bias);
+                                                  bias ? bs : nullptr, nglob);
+        if (batched) T->bias_pending[bi] = (int)g;
+        else if (bias) tr::finalize_sum_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(T->bsum, (int)g, C, bias);
     } else {
         tr::bn_back_kernel<<<grid_for((size_t)R * C), 256, 0, T->st>>>(dout, O, Y, ld, C, R, mean, sd, T->p + bn_off,
                                                                        ug, ub, dy, dres, nglob);
@@ -1425,6 +1585,7 @@ int trainer_grads(Trainer* T, const float* planes, const float* tpol, const floa
     if (B < 1 || B > T->Bmax) return fail("train: batch size out of range");
     T->last_batch = B;
     if (T->sharded && sharded_buffers(T)) return -1;
+    std::fill(T->bias_pending.begin(), T->bias_pending.end(), 0);
     AZ_HIP(hipSetDevice(T->device));
     AZ_HIP(hipEventRecord(T->ev[0], T->st));
     const int F = T->F, R = B * 64;
@@ -1465,18 +1626,33 @@ int trainer_grads(Trainer* T, const float* planes, const float* tpol, const floa
     // ---------------- forward (agent.rs:112-144, training-mode BatchNorm)
     tr::planes_kernel<<<grid_for((size_t)R * tr::X0C), 256, 0, st>>>(T->planes, B, T->x0);
     TRY(launch_conv(T, 9, T->x0, tr::X0C, tr::X0C, T->wf[0], F, T->p + L.tower[0].b, nullptr, T->y0, F, R));
-    TRY(bn_forward(T, 0, T->y0, F, F, R, L.tower[0].bn, nullptr, T->xs[0]));
+    // Winograd tower: every BatchNorm but the last is applied in the next conv's staging (BnIn);
+    // its statistics come from the producing conv's epilogue (bpart) except BN 0's
+    const bool fuse = T->wino && T->fuse_bn && T->blocks > 0;
+    TRY(bn_forward(T, 0, T->y0, F, F, R, L.tower[0].bn, nullptr, fuse ? nullptr : T->xs[0]));
     for (int b = 0; b < T->blocks; b++) {
         const auto& c1 = L.tower[1 + 2 * b];
         const auto& c2 = L.tower[2 + 2 * b];
         // Winograd convs hand their BN the per-board statistics (bpart) from their epilogue
         const float* bp = T->wino ? T->bpart : nullptr;
-        if (T->wino) TRY(launch_wino(T, T->xs[b], T->uf[1 + 2 * b], T->p + c1.b, nullptr, T->y1[b], B, 1, {T->bpart}));
-        else TRY(launch_conv(T, 9, T->xs[b], F, F, T->wf[1 + 2 * b], F, T->p + c1.b, nullptr, T->y1[b], F, R));
-        TRY(bn_forward(T, 1 + 2 * b, T->y1[b], F, F, R, c1.bn, nullptr, T->hh[b], bp));
-        if (T->wino) TRY(launch_wino(T, T->hh[b], T->uf[2 + 2 * b], T->p + c2.b, nullptr, T->y2[b], B, 1, {T->bpart}));
+        if (fuse) {   // conv1's input: BN 0 (y0) or the previous block's BN2 (y2[b-1] + xs[b-1]) -> xs[b]
+            const auto& pc = L.tower[2 * b];
+            TRY(launch_wino(T, b == 0 ? T->y0 : T->y2[b - 1], T->uf[1 + 2 * b], T->p + c1.b, nullptr, T->y1[b], B, 1,
+                            {T->bpart}, bn_in(T, 2 * b, pc.bn, b == 0 ? nullptr : T->xs[b - 1], T->xs[b])));
+        } else if (T->wino) {
+            TRY(launch_wino(T, T->xs[b], T->uf[1 + 2 * b], T->p + c1.b, nullptr, T->y1[b], B, 1, {T->bpart}));
+        } else {
+            TRY(launch_conv(T, 9, T->xs[b], F, F, T->wf[1 + 2 * b], F, T->p + c1.b, nullptr, T->y1[b], F, R));
+        }
+        TRY(bn_forward(T, 1 + 2 * b, T->y1[b], F, F, R, c1.bn, nullptr, fuse ? nullptr : T->hh[b], bp));
+        if (fuse)     // conv2's input: BN1 of this block (y1[b]) -> hh[b]
+            TRY(launch_wino(T, T->y1[b], T->uf[2 + 2 * b], T->p + c2.b, nullptr, T->y2[b], B, 1, {T->bpart},
+                            bn_in(T, 1 + 2 * b, c1.bn, nullptr, T->hh[b])));
+        else if (T->wino) TRY(launch_wino(T, T->hh[b], T->uf[2 + 2 * b], T->p + c2.b, nullptr, T->y2[b], B, 1, {T->bpart}));
         else TRY(launch_conv(T, 9, T->hh[b], F, F, T->wf[2 + 2 * b], F, T->p + c2.b, nullptr, T->y2[b], F, R));
-        TRY(bn_forward(T, 2 + 2 * b, T->y2[b], F, F, R, c2.bn, T->xs[b], T->xs[b + 1], bp));
+        // the last block's BN2 feeds the heads' 1x1 convs: applied by its own pass
+        const bool last = b == T->blocks - 1;
+        TRY(bn_forward(T, 2 + 2 * b, T->y2[b], F, F, R, c2.bn, T->xs[b], (fuse && !last) ? nullptr : T->xs[b + 1], bp));
     }
     const float* body = T->xs[T->blocks];
     const int nbn = 1 + 2 * T->blocks;
@@ -1527,34 +1703,58 @@ int trainer_grads(Trainer* T, const float* planes, const float* tpol, const floa
     // dout of every BN but the last block's second comes from a Winograd data-grad conv, whose
     // epilogue leaves the BN backward's per-board sums in bpart (dx_stats: dx came with them)
     bool dx_stats = false;
+    float* dyA = T->dy;
+    float* dyB = T->dy;
+    const bool fuseb = T->wino && T->fuse_bn;   // BN backward staged in the data-grad convs
     for (int b = T->blocks - 1; b >= 0; b--) {
         const auto& c1 = L.tower[1 + 2 * b];
         const auto& c2 = L.tower[2 + 2 * b];
         auto bstat = [&](int bi, const float* O, const float* Ybn) {
             return tr::BoardStats{T->bpart, O, Ybn, T->bmean + (size_t)bi * T->slot, T->bstd + (size_t)bi * T->slot};
         };
-        TRY(bn_backward(T, 2 + 2 * b, T->dx, T->xs[b + 1], T->y2[b], F, F, R, c2.bn, T->dy, T->dres,
+        if (fuseb) {
+            // BN2's backward (dout = dx) in conv2's data grad: dy (-> dyA, read by conv2's weight grad
+            // after it), dz (-> dres), bias partials; conv2's output dh with BN1's sums in bpart
+            tr::BnBack bb2;
+            TRY(bn_back_fused(T, 2 + 2 * b, T->dx, T->xs[b + 1], T->y2[b], R, c2.bn, dx_stats ? T->bpart : nullptr, dyA,
+                              T->dres, &bb2));
+            TRY(launch_wino(T, T->dx, T->ud[2 + 2 * b], nullptr, nullptr, T->dh, B, 2, bstat(1 + 2 * b, T->hh[b], T->y1[b]),
+                            {}, bb2));
+            TRY(launch_wino_wgrad(T, T->hh[b], dyA, B, T->g + c2.w));
+            // BN1's backward (dout = dh) in conv1's data grad (+ dres): dy -> dyB, output dxn
+            tr::BnBack bb1;
+            TRY(bn_back_fused(T, 1 + 2 * b, T->dh, T->hh[b], T->y1[b], R, c1.bn, T->bpart, dyB, nullptr, &bb1));
+            TRY(launch_wino(T, T->dh, T->ud[1 + 2 * b], nullptr, T->dres, T->dxn, B, 2,
+                            bstat(2 * b, T->xs[b], b > 0 ? T->y2[b - 1] : T->y0), {}, bb1));
+            TRY(launch_wino_wgrad(T, T->xs[b], dyB, B, T->g + c1.w));
+            dx_stats = true;
+            std::swap(T->dx, T->dxn);
+            continue;
+        }
+        TRY(bn_backward(T, 2 + 2 * b, T->dx, T->xs[b + 1], T->y2[b], F, F, R, c2.bn, dyA, T->dres,
                         dx_stats ? T->bpart : nullptr, T->g + c2.b));
-        if (T->wino) TRY(launch_wino_wgrad(T, T->hh[b], T->dy, B, T->g + c2.w));
-        else {
-            TRY(launch_wgrad(T, 9, T->hh[b], F, F, T->dy, F, F, R, T->dwtmp, T->dwtmp_cap));
+        if (T->wino) {
+            TRY(launch_wino_wgrad(T, T->hh[b], dyA, B, T->g + c2.w));
+        } else {
+            TRY(launch_wgrad(T, 9, T->hh[b], F, F, dyA, F, F, R, T->dwtmp, T->dwtmp_cap));
             tr::unpack3x3_kernel<<<grid_for((size_t)9 * F * F), 256, 0, st>>>(T->dwtmp, F, F, F, T->g + c2.w);
         }
         if (T->wino)
-            TRY(launch_wino(T, T->dy, T->ud[2 + 2 * b], nullptr, nullptr, T->dh, B, 2, bstat(1 + 2 * b, T->hh[b], T->y1[b])));
-        else TRY(launch_conv(T, 9, T->dy, F, F, T->wd[2 + 2 * b], F, nullptr, nullptr, T->dh, F, R));
-        TRY(bn_backward(T, 1 + 2 * b, T->dh, T->hh[b], T->y1[b], F, F, R, c1.bn, T->dy, nullptr,
+            TRY(launch_wino(T, dyA, T->ud[2 + 2 * b], nullptr, nullptr, T->dh, B, 2, bstat(1 + 2 * b, T->hh[b], T->y1[b])));
+        else TRY(launch_conv(T, 9, dyA, F, F, T->wd[2 + 2 * b], F, nullptr, nullptr, T->dh, F, R));
+        TRY(bn_backward(T, 1 + 2 * b, T->dh, T->hh[b], T->y1[b], F, F, R, c1.bn, dyB, nullptr,
                         T->wino ? T->bpart : nullptr, T->g + c1.b));
-        if (T->wino) TRY(launch_wino_wgrad(T, T->xs[b], T->dy, B, T->g + c1.w));
-        else {
-            TRY(launch_wgrad(T, 9, T->xs[b], F, F, T->dy, F, F, R, T->dwtmp, T->dwtmp_cap));
+        if (T->wino) {
+            TRY(launch_wino_wgrad(T, T->xs[b], dyB, B, T->g + c1.w));
+        } else {
+            TRY(launch_wgrad(T, 9, T->xs[b], F, F, dyB, F, F, R, T->dwtmp, T->dwtmp_cap));
             tr::unpack3x3_kernel<<<grid_for((size_t)9 * F * F), 256, 0, st>>>(T->dwtmp, F, F, F, T->g + c1.w);
         }
         // dx is the gradient of block b's input: the output of BN 2b (BN 0 = the input conv's)
         if (T->wino)
-            TRY(launch_wino(T, T->dy, T->ud[1 + 2 * b], nullptr, T->dres, T->dxn, B, 2, bstat(2 * b, T->xs[b],
-                                                                                            b > 0 ? T->y2[b - 1] : T->y0)));
-        else TRY(launch_conv(T, 9, T->dy, F, F, T->wd[1 + 2 * b], F, nullptr, T->dres, T->dxn, F, R));
+            TRY(launch_wino(T, dyB, T->ud[1 + 2 * b], nullptr, T->dres, T->dxn, B, 2, bstat(2 * b, T->xs[b],
+                                                                                          b > 0 ? T->y2[b - 1] : T->y0)));
+        else TRY(launch_conv(T, 9, dyB, F, F, T->wd[1 + 2 * b], F, nullptr, T->dres, T->dxn, F, R));
         dx_stats = T->wino;
         std::swap(T->dx, T->dxn);
     }
@@ -1563,6 +1763,20 @@ int trainer_grads(Trainer* T, const float* planes, const float* tpol, const floa
                     T->g + L.tower[0].b));
     TRY(launch_wgrad(T, 9, T->x0, tr::X0C, tr::X0C, T->dy, F, F, R, T->dwtmp, T->dwtmp_cap));
     tr::unpack3x3_kernel<<<grid_for((size_t)9 * 19 * F), 256, 0, st>>>(T->dwtmp, F, 19, tr::X0C, T->g + L.tower[0].w);
+    if (!T->bias_pending.empty()) {   // the tower's conv bias gradients: one launch for BNs 1..2B
+        const int nt = (int)T->bias_pending.size();
+        bool same = nt > 1;
+        for (int j = 1; j < nt; j++) same = same && T->bias_pending[j] == T->bias_pending[1];
+        const int j0 = same ? 1 : 0;
+        if (same && T->bias_pending[1] > 0)
+            tr::finalize_sum_batched_kernel<<<dim3(tr::finalize_grid(F), nt - 1), 256, 0, st>>>(
+                T->bsum_all + T->bsum_stride, T->bsum_stride, T->bias_pending[1], F, T->bias_dst + 1, T->g);
+        for (int j = same ? 0 : j0; j < (same ? 1 : nt); j++)
+            if (T->bias_pending[j] > 0)
+                tr::finalize_sum_kernel<<<tr::finalize_grid(F), 256, 0, st>>>(
+                    T->bsum_all + (size_t)j * T->bsum_stride, T->bias_pending[j], F, T->g + L.tower[j].b);
+        std::fill(T->bias_pending.begin(), T->bias_pending.end(), 0);
+    }
     AZ_HIP(hipMemcpyAsync(T->hloss, T->loss, (size_t)B * 2 * sizeof(float), hipMemcpyDeviceToHost, st));
     AZ_HIP(hipStreamSynchronize(st));
     double pl = 0.0, vl = 0.0;
@@ -1723,12 +1937,17 @@ int az_trainer_create(int blocks, int filters, const float* weights, size_t n, i
     if (T->wino) {   // Winograd weight grads: [16][Bmax * 16][F] transforms, dU [16][F][F]
         wp = std::max(wp, wino_gemm_splits(max_batch) * 16 * (size_t)F * F);
     }
-    T->wpart = A(wp);
     T->wpart_cap = wp;
+    T->wpart = A(wp);
     T->cpart = A((R / tr::CS_ROWS + 2) * 2 * (size_t)std::max(F, 65));
     T->bpart = A((size_t)max_batch * 2 * F);
     T->bsum_cap = (size_t)256 * 4 * 2 * std::max(F, 64);   // bn_grid's workgroup cap x [2][C]
     T->bsum = A(T->bsum_cap);
+    if (T->wino) {   // per-BN bias partials of the tower (batched finalize) and the second dy
+        T->bsum_stride = T->bsum_cap;
+        T->bsum_all = A((size_t)nconv * T->bsum_stride);
+        T->bias_pending.assign(nconv, 0);
+    }
     // dW scratch: input conv [9][64][F], residual conv [9][F][F], heads [F][64] + its [40][F]
     // transpose, policy_conv_2 [32][64], value_linear_2 partial sums (65)
     T->dwtmp_cap = std::max({(size_t)9 * 64 * F, (size_t)9 * F * F, (size_t)F * 64 + 40 * (size_t)F, (size_t)32 * 64,
@@ -1737,6 +1956,7 @@ int az_trainer_create(int blocks, int filters, const float* weights, size_t n, i
     T->planes = A((size_t)max_batch * 19 * 64); T->tpol = A((size_t)max_batch * 4096); T->tval = A(max_batch);
     T->loss = A((size_t)max_batch * 2); T->vpart = A((size_t)max_batch * 65);
     ok = ok && hipHostMalloc((void**)&T->hloss, (size_t)max_batch * 2 * sizeof(float), 0) == hipSuccess;
+    if (const char* e = getenv("AZ_TRAIN_FUSE_BN")) T->fuse_bn = atoi(e) != 0;
     if (!ok) { delete T; return fail("az_trainer_create: out of device memory"); }
     // parameters, zero moments, trainable mask (BatchNorm running statistics are not parameters)
     std::vector<uint8_t> mask(T->np, 1);
@@ -1748,6 +1968,15 @@ int az_trainer_create(int blocks, int filters, const float* weights, size_t n, i
     bn_stats(T->L.pbn, 32);
     bn_stats(T->L.vbn, 8);
     T->nstat = (int)sidx.size();
+    if (T->wino) {
+        std::vector<uint32_t> bd;
+        for (const auto& c : T->L.tower) bd.push_back((uint32_t)c.b);
+        T->bias_dst = reinterpret_cast<uint32_t*>(T->alloc(bd.size()));
+        if (!T->bias_dst || hipMemcpy(T->bias_dst, bd.data(), bd.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+            delete T;
+            return fail("az_trainer_create: out of device memory");
+        }
+    }
     T->stat_idx = reinterpret_cast<uint32_t*>(T->alloc(sidx.size()));
     T->stat_buf = T->alloc(sidx.size());
     if (!T->stat_idx || !T->stat_buf) { delete T; return fail("az_trainer_create: out of device memory"); }
