@@ -303,7 +303,11 @@ __device__ __forceinline__ void heads_group(const char* __restrict__ xb, float* 
     if constexpr (WIDE) {
 #pragma unroll
         for (int i = 0; i < KP / 4; i++)
+#ifdef AZ_HEADS_NOVFC   // timing-only bound (wrong values): no value-FC weight stream
+            wq[i] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#else
             wq[i] = *reinterpret_cast<const f32x4*>(head + L.l1w + (size_t)(w * KP + 4 * i + h) * 64 + 4 * l16);
+#endif
     } else {
 #pragma unroll
         for (int i = 0; i < KPRE; i++) wv[i] = head[L.l1w + (size_t)(w * KP + i) * 64 + lane];
