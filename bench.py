@@ -131,9 +131,10 @@ def train_child(a):
         pol[i, idx] = v / v.sum()
     val = rng.uniform(-1, 1, B).astype(np.float32)
     sharded = a.train_mode == "sharded"
-    if sharded:      # this rank's shard of the one global batch (the first B / world rows)
+    if sharded:      # this rank's shard of the one global batch (every rank generated all of it)
         B //= a.world
-        planes, pol, val = planes[:B], pol[:B], val[:B]
+        sl = slice(a.rank * B, (a.rank + 1) * B)
+        planes, pol, val = planes[sl], pol[sl], val[sl]
     tr = A.Trainer(a.blocks, a.filters, max_batch=B, device=a.device, seed=42)
     if a.world > 1 or sharded:     # sharded at world 1: the 1-rank communicator, so its collectives are timed
         tr.set_comm(bytes.fromhex(a.uid) if a.uid != "-" else A.comm_unique_id(), a.rank, a.world)
