@@ -385,7 +385,8 @@ def test_sharded_world1_rccl_is_the_plain_step(require_gpu, blocks, filters):
         assert np.array_equal(a.params(), b.params())
 
 
-def test_sharded_world2_host_reducer_matches_single_batch(require_gpu):
+@pytest.mark.parametrize("split", [256, 200])
+def test_sharded_world2_host_reducer_matches_single_batch(require_gpu, split):
     """the reference trains ONE batch of 512 (training.rs:137-159,
     parameters.rs:17) with batch-512 BatchNorm statistics (agent.rs:37,41,115).  Two ranks in
     sharded mode (az_trainer_set_sharded, exchanges through the host reducer), 256 positions each,
@@ -395,25 +396,28 @@ def test_sharded_world2_host_reducer_matches_single_batch(require_gpu):
       every gradient tensor            <= 1e-4 relative norm vs the oracle (sharded: g0 + g1)
       sharded vs 1-rank, per tensor    <= 1e-2 relative norm (different ReLU branches near 0)
       running statistics               <= 1e-5 vs the oracle; bit-identical on the two ranks
-    then the AdamW step: both ranks bit-identical and equal to T.adamw_step(p, g0 + g1, world=1)."""
+    then the AdamW step: both ranks bit-identical and equal to T.adamw_step(p, g0 + g1, world=1).
+    split = 200: unequal shards (200 + 312 positions; the Chan combine weights each rank by its rows,
+    the loss and BN backward divide by the global count)."""
     blocks, filters, n = 2, 256, 512
-    h = n // 2
+    cuts = [0, split, n]
     w = A.random_weights(blocks, filters, seed=41)
     planes, tpol, tval = batch(n, seed=42)
     one = A.Trainer(blocks, filters, weights=w, max_batch=n)
     l1 = one.compute_gradients(planes, tpol, tval)
     g1, p1, m1 = one.grads(), one.params(), one.relu_masks(n)
-    ranks = [A.Trainer(blocks, filters, weights=w, max_batch=h) for _ in range(2)]
+    ranks = [A.Trainer(blocks, filters, weights=w, max_batch=cuts[r + 1] - cuts[r]) for r in range(2)]
     red = _host_reducer_pair()
     for r, tr in enumerate(ranks):
         tr.set_host_reducer(red(r), r, 2)
         tr.set_sharded(True)
-    ls = _run_ranks([lambda r=r, tr=tr: tr.compute_gradients(planes[r * h:(r + 1) * h], tpol[r * h:(r + 1) * h],
-                                                             tval[r * h:(r + 1) * h]) for r, tr in enumerate(ranks)])
+    sl = [slice(cuts[r], cuts[r + 1]) for r in range(2)]
+    ls = _run_ranks([lambda r=r, tr=tr: tr.compute_gradients(planes[sl[r]], tpol[sl[r]], tval[sl[r]])
+                     for r, tr in enumerate(ranks)])
     assert ls[0] == ls[1]                     # global means on both ranks
     gs = [tr.grads() for tr in ranks]
     ps = [tr.params() for tr in ranks]
-    ms = [tr.relu_masks(h) for tr in ranks]
+    ms = [tr.relu_masks(cuts[r + 1] - cuts[r]) for r, tr in enumerate(ranks)]
     msh = [np.concatenate([a, b]) for a, b in zip(ms[0], ms[1])]
     gsh = gs[0].astype(np.float64) + gs[1].astype(np.float64)
     stats = ~T.trainable_mask(blocks, filters)
