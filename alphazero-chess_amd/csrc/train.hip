@@ -252,7 +252,11 @@ constexpr int WG_SX = 256, WG_SD = 256 + 16;
 // row or column -> a - b, a + b, b - a, a - b (B^T rows)
 __device__ __forceinline__ f32x4 wino_comb(int k, f32x4 a, f32x4 b) { return k == 1 ? a + b : k == 2 ? b - a : a - b; }
 // (16 waves of 16 output channels each, 4 per SIMD at <= 128 VGPRs, measured the same: 166.1 vs
-// 166.7 us, profiles/r04g_train_kernel_stats_w16.csv; not kept)
+// 166.7 us, profiles/r04g_train_kernel_stats_w16.csv; not kept.  Round 5: double-buffered staging
+// with one barrier per board, the next board's transform between the row quads' MFMAs -- 22.68 /
+// 22.57 ms per step (transform mid-board / after the last quad) against 22.35 -- and a
+// branch-free sign-mask form of wino_comb, 23.21: both spill (4-12 VGPRs) at the 256-VGPR cap;
+// profiles/r05h_train_ab.txt.  Not kept.)
 __global__ void __launch_bounds__(512)
 wino_wgrad_gemm_kernel(const float* __restrict__ X, const float* __restrict__ DY, int K, int rows_per_split,
                        float* __restrict__ partial) {
