@@ -1707,8 +1707,7 @@ int trainer_grads(Trainer* T, const float* planes, const float* tpol, const floa
     // dout of every BN but the last block's second comes from a Winograd data-grad conv, whose
     // epilogue leaves the BN backward's per-board sums in bpart (dx_stats: dx came with them)
     bool dx_stats = false;
-    float* dyA = T->dy;
-    float* dyB = T->dy;
+    float* const dy = T->dy;   // each BN backward's dy: read by its conv's weight grad, then overwritten
     const bool fuseb = T->wino && T->fuse_bn;   // BN backward staged in the data-grad convs
     for (int b = T->blocks - 1; b >= 0; b--) {
         const auto& c1 = L.tower[1 + 2 * b];
@@ -1717,48 +1716,48 @@ int trainer_grads(Trainer* T, const float* planes, const float* tpol, const floa
             return tr::BoardStats{T->bpart, O, Ybn, T->bmean + (size_t)bi * T->slot, T->bstd + (size_t)bi * T->slot};
         };
         if (fuseb) {
-            // BN2's backward (dout = dx) in conv2's data grad: dy (-> dyA, read by conv2's weight grad
+            // BN2's backward (dout = dx) in conv2's data grad: dy (read by conv2's weight grad
             // after it), dz (-> dres), bias partials; conv2's output dh with BN1's sums in bpart
             tr::BnBack bb2;
-            TRY(bn_back_fused(T, 2 + 2 * b, T->dx, T->xs[b + 1], T->y2[b], R, c2.bn, dx_stats ? T->bpart : nullptr, dyA,
+            TRY(bn_back_fused(T, 2 + 2 * b, T->dx, T->xs[b + 1], T->y2[b], R, c2.bn, dx_stats ? T->bpart : nullptr, dy,
                               T->dres, &bb2));
             TRY(launch_wino(T, T->dx, T->ud[2 + 2 * b], nullptr, nullptr, T->dh, B, 2, bstat(1 + 2 * b, T->hh[b], T->y1[b]),
                             {}, bb2));
-            TRY(launch_wino_wgrad(T, T->hh[b], dyA, B, T->g + c2.w));
-            // BN1's backward (dout = dh) in conv1's data grad (+ dres): dy -> dyB, output dxn
+            TRY(launch_wino_wgrad(T, T->hh[b], dy, B, T->g + c2.w));
+            // BN1's backward (dout = dh) in conv1's data grad (+ dres): dy, output dxn
             tr::BnBack bb1;
-            TRY(bn_back_fused(T, 1 + 2 * b, T->dh, T->hh[b], T->y1[b], R, c1.bn, T->bpart, dyB, nullptr, &bb1));
+            TRY(bn_back_fused(T, 1 + 2 * b, T->dh, T->hh[b], T->y1[b], R, c1.bn, T->bpart, dy, nullptr, &bb1));
             TRY(launch_wino(T, T->dh, T->ud[1 + 2 * b], nullptr, T->dres, T->dxn, B, 2,
                             bstat(2 * b, T->xs[b], b > 0 ? T->y2[b - 1] : T->y0), {}, bb1));
-            TRY(launch_wino_wgrad(T, T->xs[b], dyB, B, T->g + c1.w));
+            TRY(launch_wino_wgrad(T, T->xs[b], dy, B, T->g + c1.w));
             dx_stats = true;
             std::swap(T->dx, T->dxn);
             continue;
         }
-        TRY(bn_backward(T, 2 + 2 * b, T->dx, T->xs[b + 1], T->y2[b], F, F, R, c2.bn, dyA, T->dres,
+        TRY(bn_backward(T, 2 + 2 * b, T->dx, T->xs[b + 1], T->y2[b], F, F, R, c2.bn, dy, T->dres,
                         dx_stats ? T->bpart : nullptr, T->g + c2.b));
         if (T->wino) {
-            TRY(launch_wino_wgrad(T, T->hh[b], dyA, B, T->g + c2.w));
+            TRY(launch_wino_wgrad(T, T->hh[b], dy, B, T->g + c2.w));
         } else {
-            TRY(launch_wgrad(T, 9, T->hh[b], F, F, dyA, F, F, R, T->dwtmp, T->dwtmp_cap));
+            TRY(launch_wgrad(T, 9, T->hh[b], F, F, dy, F, F, R, T->dwtmp, T->dwtmp_cap));
             tr::unpack3x3_kernel<<<grid_for((size_t)9 * F * F), 256, 0, st>>>(T->dwtmp, F, F, F, T->g + c2.w);
         }
         if (T->wino)
-            TRY(launch_wino(T, dyA, T->ud[2 + 2 * b], nullptr, nullptr, T->dh, B, 2, bstat(1 + 2 * b, T->hh[b], T->y1[b])));
-        else TRY(launch_conv(T, 9, dyA, F, F, T->wd[2 + 2 * b], F, nullptr, nullptr, T->dh, F, R));
-        TRY(bn_backward(T, 1 + 2 * b, T->dh, T->hh[b], T->y1[b], F, F, R, c1.bn, dyB, nullptr,
+            TRY(launch_wino(T, dy, T->ud[2 + 2 * b], nullptr, nullptr, T->dh, B, 2, bstat(1 + 2 * b, T->hh[b], T->y1[b])));
+        else TRY(launch_conv(T, 9, dy, F, F, T->wd[2 + 2 * b], F, nullptr, nullptr, T->dh, F, R));
+        TRY(bn_backward(T, 1 + 2 * b, T->dh, T->hh[b], T->y1[b], F, F, R, c1.bn, dy, nullptr,
                         T->wino ? T->bpart : nullptr, T->g + c1.b));
         if (T->wino) {
-            TRY(launch_wino_wgrad(T, T->xs[b], dyB, B, T->g + c1.w));
+            TRY(launch_wino_wgrad(T, T->xs[b], dy, B, T->g + c1.w));
         } else {
-            TRY(launch_wgrad(T, 9, T->xs[b], F, F, dyB, F, F, R, T->dwtmp, T->dwtmp_cap));
+            TRY(launch_wgrad(T, 9, T->xs[b], F, F, dy, F, F, R, T->dwtmp, T->dwtmp_cap));
             tr::unpack3x3_kernel<<<grid_for((size_t)9 * F * F), 256, 0, st>>>(T->dwtmp, F, F, F, T->g + c1.w);
         }
         // dx is the gradient of block b's input: the output of BN 2b (BN 0 = the input conv's)
         if (T->wino)
-            TRY(launch_wino(T, dyB, T->ud[1 + 2 * b], nullptr, T->dres, T->dxn, B, 2, bstat(2 * b, T->xs[b],
+            TRY(launch_wino(T, dy, T->ud[1 + 2 * b], nullptr, T->dres, T->dxn, B, 2, bstat(2 * b, T->xs[b],
                                                                                           b > 0 ? T->y2[b - 1] : T->y0)));
-        else TRY(launch_conv(T, 9, dyB, F, F, T->wd[1 + 2 * b], F, nullptr, T->dres, T->dxn, F, R));
+        else TRY(launch_conv(T, 9, dy, F, F, T->wd[1 + 2 * b], F, nullptr, T->dres, T->dxn, F, R));
         dx_stats = T->wino;
         std::swap(T->dx, T->dxn);
     }
