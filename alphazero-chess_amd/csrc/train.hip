@@ -14,9 +14,13 @@
 // gradients are clipped by value to [-1, 1] and applied with burn's AdamW (training.rs:63-66:
 // beta 0.9 / 0.999, eps 1e-5 outside the sqrt, decoupled weight decay 1e-4).
 // Every reduction has a fixed order, so a step is bit-reproducible run to run.
+// At F = 256 the residual convs run as Winograd F(2x2,3x3) (wino.h), each BatchNorm's apply staged
+// in the next conv and its backward in the next data-grad conv (tr::BnIn / tr::BnBack).
 // Data-parallel (training.rs:137-190 on N GPUs): the flat gradient is summed over
-// ranks with ncclAllReduce (RCCL over xGMI) on the trainer's stream before clipping; BatchNorm
-// running statistics are averaged the same way after the step.
+// ranks with ncclAllReduce (RCCL over xGMI) on the trainer's stream before clipping.  Per-rank
+// batches (default): BatchNorm running statistics are averaged the same way after the step.
+// Sharded batch (az_trainer_set_sharded): the ranks' batches are one batch, every BatchNorm's
+// statistics and backward sums are exchanged inside the step (bn_local / bn_global kernels).
 #include <math.h>
 #include <string.h>
 
