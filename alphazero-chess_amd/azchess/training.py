@@ -256,7 +256,7 @@ class Trainer:
 
 def train(iterations, blocks=NUM_RES_BLOCKS, filters=NUM_FILTERS, games=NUM_EPISODES, sims=NUM_SIMULATIONS,
           min_replay=MIN_REPLAY_SIZE, train_steps=NUM_TRAIN_STEPS, batch_size=BATCH_SIZE, replay=None, trainer=None,
-          device=0, seed=SEED, dtype="f32", comm=None, shard_batch=False, log=None):
+          device=0, seed=SEED, dtype="f32", comm=None, shard_batch=False, reducer=None, log=None):
     """train() (training.rs:39-275) without the TUI, arena and Elo (SKIP_VALIDATION = true,
     parameters.rs:35): per iteration, self-play `games` games with model.valid() until the replay
     buffer holds min_replay unique positions, then train_steps AdamW steps on batches of
@@ -266,10 +266,13 @@ def train(iterations, blocks=NUM_RES_BLOCKS, filters=NUM_FILTERS, games=NUM_EPIS
     step is the reference's ONE batch of batch_size split over the ranks (batch_size / world per
     rank, az_trainer_set_sharded: BatchNorm statistics over the whole batch); without it every
     rank trains its own batch_size (global batch batch_size x world, per-rank BatchNorm).
+    reducer = (reduce, rank, world) instead of comm: the same exchanges through a host callback
+    (Trainer.set_host_reducer; e.g. gloo, or ranks as threads of one process).
     Returns (trainer, replay, per-iteration stats)."""
     from .memory import ReplayBuffer
-    rank = comm[1] if comm else 0
-    world = comm[2] if comm else 1
+    if comm and reducer:
+        raise ValueError("train: comm (RCCL) or reducer (host), not both")
+    rank, world = (comm[1], comm[2]) if comm else (reducer[1], reducer[2]) if reducer else (0, 1)
     if shard_batch and batch_size % world:
         raise ValueError("shard_batch: batch_size %d is not a multiple of world %d" % (batch_size, world))
     local_batch = batch_size // world if shard_batch else batch_size
@@ -277,6 +280,8 @@ def train(iterations, blocks=NUM_RES_BLOCKS, filters=NUM_FILTERS, games=NUM_EPIS
         trainer = Trainer(blocks, filters, max_batch=local_batch, device=device, seed=seed)
         if comm:
             trainer.set_comm(*comm)
+        elif reducer:
+            trainer.set_host_reducer(*reducer)
         if shard_batch:
             trainer.set_sharded(True)
     replay = replay if replay is not None else ReplayBuffer()

@@ -457,3 +457,20 @@ def test_sharded_world2_host_reducer_matches_single_batch(require_gpu, split):
     got0, got1 = ranks[0].params(), ranks[1].params()
     assert np.array_equal(got0, got1)
     assert np.array_equal(got0, want), np.abs(got0 - want).max()
+
+
+def test_train_loop_sharded_two_ranks_host_reducer(require_gpu):
+    """train(shard_batch=True) (training.rs:71-200 with the reference's one batch split over the
+    ranks) for two ranks as threads on one GPU, exchanges through a host reducer: each rank plays its
+    own games into its own replay buffer and samples batch_size / 2 positions per step; the sharded
+    steps apply the same update on both ranks, so the two trainers end with bit-identical
+    parameters (BatchNorm running statistics included), and the losses are finite global means."""
+    red = _host_reducer_pair()
+    out = _run_ranks([lambda r=r: A.train(1, blocks=2, filters=256, games=16, sims=8, min_replay=64, train_steps=3,
+                                          batch_size=64, seed=5, reducer=(red(r), r, 2), shard_batch=True)
+                      for r in range(2)])
+    (t0, rep0, h0), (t1, rep1, h1) = out
+    assert h0[0]["policy_loss"] == h1[0]["policy_loss"] and h0[0]["value_loss"] == h1[0]["value_loss"]
+    assert np.isfinite(h0[0]["policy_loss"]) and np.isfinite(h0[0]["value_loss"])
+    assert np.array_equal(t0.params(), t1.params())
+    assert len(rep0) >= 64 and len(rep1) >= 64
