@@ -79,6 +79,13 @@ constexpr int WINO_PAD_SQ = 8;
 //   WINO_TSTAG 16  steps by which the second wave of each SIMD pair delays its transform (-0.4 %)
 //   WINO_LA 4      B fragments read ahead from V
 constexpr int WINO_TSPLIT = 2, WINO_TSTAG = 16, WINO_LA = 4;
+// timing-only knob (wrong results): -DAZ_WINO_WFAKE=1 makes every ring step re-read the first two
+// steps' weights (L2 / L1 hits), to price the weight stream from L2
+#if defined(AZ_WINO_WFAKE) && AZ_WINO_WFAKE
+#define WINO_WSTEP(t) ((t) & 1)
+#else
+#define WINO_WSTEP(t) (t)
+#endif
 
 // Per filter count: NWV waves per workgroup, NN 16-channel output fragments per wave, XS points
 // per ring step, CH input channels per transform chunk (V buffer = CH KB), PF ring steps of
@@ -383,7 +390,7 @@ __device__ __forceinline__ void wino_core(char* __restrict__ ldsb, int vbase,
                     for (int n = 0; n < NN; n++)
                         wr[st % PF][xs][n] = __builtin_bit_cast(
                             f32x4, __builtin_amdgcn_raw_buffer_load_b128(nxt ? rN : rW, voff + n * 1024,
-                                                                         (to + xs) * CF * 1024, 0));
+                                                                         WINO_WSTEP(to + xs) * CF * 1024, 0));
             }
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
