@@ -236,29 +236,6 @@ def test_winograd_training_convs_match_direct(require_gpu, monkeypatch):
         assert np.linalg.norm(g1[o:o + cnt] - r) <= 1e-2 * max(np.linalg.norm(r), 1e-30), name
 
 
-@pytest.mark.parametrize("blocks,n,fuse", [(20, 4, "1"), (2, 80, "1"), (2, 80, "0"), (3, 13, "0")])
-def test_half_workgroup_convs_bit_identical(require_gpu, monkeypatch, blocks, n, fuse):
-    """The training step's Winograd convs as two half-channel workgroups per board
-    (conv_wino_half_kernel, AZ_TRAIN_HALF=1) and as one workgroup per board (conv_wino_train_kernel,
-    the default): the same MFMA accumulation order, transforms, BatchNorm staging and per-board
-    statistics, so two steps give bit-identical losses, gradients and parameters.  n = 80 maps both
-    halves of a board to one XCD (n % 8 == 0), n = 4 / 13 take the plain board order; fuse = "0" runs
-    the convs without BatchNorm staging (AZ_TRAIN_FUSE_BN=0)."""
-    w = A.random_weights(blocks, 256, seed=17)
-    planes, tpol, tval = batch(n, seed=300 + n)
-    monkeypatch.setenv("AZ_TRAIN_FUSE_BN", fuse)
-    out = {}
-    for flag in ("1", "0"):
-        monkeypatch.setenv("AZ_TRAIN_HALF", flag)
-        tr = A.Trainer(blocks, 256, weights=w, max_batch=n)
-        losses = [tr.step(planes, tpol, tval, A.get_cyclical_lr(it)) for it in range(2)]
-        out[flag] = (losses, tr.grads(), tr.params())
-    (l1, g1, p1), (l0, g0, p0) = out["1"], out["0"]
-    assert l1 == l0
-    assert np.array_equal(g1, g0), np.abs(g1 - g0).max()
-    assert np.array_equal(p1, p0), np.abs(p1 - p0).max()
-
-
 def test_winograd_weight_grad_multi_split(require_gpu):
     """the production Winograd weight grad (wino_wgrad_gemm_kernel, 512 rows of
     (board, tile) per split, the splits summed by wino_wgrad_reduce_out_kernel) with more than one

@@ -36,9 +36,7 @@ buf = np.zeros(NL * NB * 8, np.uint64)
 assert rd(buf.ctypes.data, buf.size, C.byref(n)) == 0
 buf = buf.reshape(NL, NB, 8).astype(np.int64)
 tot = {}
-half = os.environ.get("AZ_TRAIN_HALF", "0") != "0"
-NW = 2 * B if half else B       # workgroups per launch
-print("workgroups per launch:", NW, "(half-channel kernel)" if half else "(one board each)")
+NW = B                          # workgroups per launch (one board each)
 for k in range(counts[-1] - per_step, counts[-1]):
     t = buf[k % NL, :NW]
     # each XCD has its own shader clock: the span per XCD, the longest
@@ -52,7 +50,7 @@ for k in range(counts[-1] - per_step, counts[-1]):
     cs, ts, te = cu[order], t[order, 0], t[order, 3]
     same = cs[1:] == cs[:-1]
     gap = (ts[1:] - te[:-1])[same]
-    # per CU: workgroup time over the union of its workgroups' intervals (2 = two always resident)
+    # per CU: workgroup time over the union of its workgroups' intervals (how many were resident)
     conc = []
     for u in np.unique(cs):
         a_, b_ = ts[cs == u], te[cs == u]
