@@ -111,9 +111,10 @@ int az_pos_from_fen(const char* fen, az_pos* out) {
     p.halfmoves = (uint16_t)hm;
     p.fullmoves = (uint16_t)(fm < 1 ? 1 : fm);
     p.ep = azc::pseudo_ep(p, ep);
+    // validated before finalize, whose move generator assumes one king per side
+    if (const char* why = azc::setup_error(p)) return fail(std::string("FEN rejected (") + why + "): " + fen);
     bool chk;
     azc::finalize(p, &chk);
-    if (const char* why = azc::setup_error(p)) return fail(std::string("FEN rejected (") + why + "): " + fen);
     P(out) = p;
     return 0;
 }

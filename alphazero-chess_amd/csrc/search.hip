@@ -758,10 +758,10 @@ int upload_histories(az_search* s, const az_pos* start, const int32_t* hist, con
         azc::Pos p = azc::startpos();
         if (start) {
             p = *reinterpret_cast<const azc::Pos*>(start + g);
+            if (const char* why = azc::setup_error(p))   // before finalize: its generator assumes one king per side
+                return fail("root start position of game " + std::to_string(g) + " rejected: " + why);
             bool chk;
             azc::finalize(p, &chk);          // flags / rep_key from the position itself
-            if (const char* why = azc::setup_error(p))
-                return fail("root start position of game " + std::to_string(g) + " rejected: " + why);
         }
         std::vector<azc::Pos> H{p};
         const int b = off ? off[g] : 0, e = off ? off[g + 1] : 0;
