@@ -706,7 +706,7 @@ __global__ void bn_back_kernel(const float* __restrict__ dout, const float* __re
                                const float* __restrict__ dbeta, float* __restrict__ dy, float* __restrict__ dres,
                                const float* __restrict__ nglob) {
     const size_t n = (size_t)R * C;
-    const float invR = 1.0f / (nglob ? *nglob : (float)R);
+    const float invR = 1.0f / (nglob ? nglob[vgpr_index(0)] : (float)R);
     for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
         const int r = (int)(e / C), c = (int)(e % C);
         const size_t o = (size_t)r * ld + c;
@@ -727,7 +727,7 @@ __global__ void __launch_bounds__(256) bn_back4_kernel(const float* __restrict__
                                                        const float* __restrict__ nglob) {
     const int cq = C / 4, c = 4 * (threadIdx.x % cq), rs = 256 / cq;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);   // bsum: this thread's rows of dy, in order
-    const float invR = 1.0f / (nglob ? *nglob : (float)R);   // sharded batch: all ranks' rows
+    const float invR = 1.0f / (nglob ? nglob[vgpr_index(0)] : (float)R);   // sharded batch: all ranks' rows (vector load)
     const float4 mu = *reinterpret_cast<const float4*>(mean + c), sd = *reinterpret_cast<const float4*>(stdv + c);
     const float4 ga = *reinterpret_cast<const float4*>(gamma + c), dg = *reinterpret_cast<const float4*>(dgamma + c);
     const float4 db = *reinterpret_cast<const float4*>(dbeta + c);
@@ -827,7 +827,7 @@ loss_kernel(const float* __restrict__ logits, const float* __restrict__ tpol, co
 #pragma unroll
     for (int j = 0; j < 16; j++) { l[j] = expf(l[j] - mx); se += l[j]; }
     se = block_reduce(se, false);
-    const float invB = 1.0f / (nglob ? *nglob / 64.0f : (float)B);   // sharded: the global batch
+    const float invB = 1.0f / (nglob ? nglob[vgpr_index(0)] / 64.0f : (float)B);   // sharded: the global batch (vector load)
     float lp = 0.0f, pg = 0.0f, G[16];
 #pragma unroll
     for (int j = 0; j < 16; j++) {
