@@ -1123,35 +1123,41 @@ __global__ void repack3x3_kernel(const float* __restrict__ w, int co_n, int ci_n
 // The split reduction and dW = G^T dU G in one pass: dU[xi][e] = sum over splits s (in order) of
 // partial[s][xi][e], e = ci F + co, then dW[co][ci] = G^T dU G in f64, rounded once, into the
 // gradient's burn layout g[co][ci][3][3] (bit-identical to the round-3 reduce_kernel + separate
-// transform, 13.4 + 5.7 us per conv, without the dU round trip).  Workgroup = 64 e (lanes) x NW
-// waves, wave w = points w, w + NW, ...: each thread's split loads per point are independent (16
-// waves of one point: 15.5 us alone; 4 points per wave measured 23.2 us: too few loads in flight),
-// the points meet in LDS, waves 0-2 write kernel row ky.  (Round 5: NW = 4 -- 256 threads, which
+// transform, 13.4 + 5.7 us per conv, without the dU round trip).  Workgroup = 64 lanes x 4
+// consecutive e x 16 waves, wave = point: each thread's split loads are independent 16-byte loads
+// (round 5: 13.9 us per conv against 15.5 with one e per lane, bit-identical; a 4 ci x 64 co tile
+// written as contiguous runs per co measured 23.4: too few workgroups), the points meet in LDS,
+// waves 0-11 = (element of the four, kernel row ky).  (Round 5: a 256-thread form -- which would
 // fit beside a Winograd conv workgroup on its CU -- on a second stream beside the next data-grad
 // conv measured slower than in sequence, 22.72 vs 22.20 ms per step, as did the whole weight grad
 // on a second stream (22.67 vs 22.62): its 256-VGPR workgroups hold their CUs for the whole GEMM,
 // so the data-grad chain's small kernels queued behind them.  Not kept.)
-template <int NW>
-__global__ void __launch_bounds__(64 * NW) wino_wgrad_reduce_out_kernel(const float* __restrict__ partial, int splits,
-                                                                        int F, float* __restrict__ g) {
-    __shared__ float su[16][64];
+__global__ void __launch_bounds__(1024) wino_wgrad_reduce_out_kernel(const float* __restrict__ partial, int splits,
+                                                                      int F, float* __restrict__ g) {
+    __shared__ float4 su[16][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const size_t n = (size_t)F * F, e = (size_t)blockIdx.x * 64 + lane;
-#pragma unroll
-    for (int xi = w; xi < 16; xi += NW) {
-        float s = 0.0f;
-        for (int k = 0; k < splits; k++) s += partial[((size_t)k * 16 + xi) * n + e];
+    const size_t n4 = (size_t)F * F / 4, e4 = (size_t)blockIdx.x * 64 + lane;
+    const float4* P4 = reinterpret_cast<const float4*>(partial);
+    {
+        const int xi = w;
+        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int k = 0; k < splits; k++) {
+            const float4 v = P4[((size_t)k * 16 + xi) * n4 + e4];
+            s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+        }
         su[xi][lane] = s;
     }
     __syncthreads();
-    if (w >= 3) return;
-    const int ky = w, co = (int)(e % F), ci = (int)(e / F);
+    if (w >= 12) return;
+    const int ky = w % 3, part = w / 3;   // wave: kernel row ky of element part of the lane's four
+    const size_t e = e4 * 4 + part;
+    const int co = (int)(e % F), ci = (int)(e / F);
     const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
+    auto u = [&](int x) { const float4 q = su[x][lane]; return (double)(part == 0 ? q.x : part == 1 ? q.y : part == 2 ? q.z : q.w); };
     double tg[4];
 #pragma unroll
     for (int j = 0; j < 4; j++)
-        tg[j] = G[0][ky] * (double)su[j][lane] + G[1][ky] * (double)su[4 + j][lane] + G[2][ky] * (double)su[8 + j][lane] +
-                G[3][ky] * (double)su[12 + j][lane];
+        tg[j] = G[0][ky] * u(j) + G[1][ky] * u(4 + j) + G[2][ky] * u(8 + j) + G[3][ky] * u(12 + j);
 #pragma unroll
     for (int kx = 0; kx < 3; kx++)
         g[((size_t)co * F + ci) * 9 + ky * 3 + kx] =
@@ -1418,10 +1424,10 @@ int launch_wino_wgrad(Trainer* T, const float* X, const float* DY, int B, float*
     const int splits = (int)wino_gemm_splits(B);
     if (splits * 16 * (size_t)F * F > T->wpart_cap) return fail("Winograd wgrad: partial buffer too small");
     if ((size_t)B * 64 * F * 4 >= (size_t)0x40000000) return fail("Winograd wgrad: batch too large for 32-bit offsets");
-    if ((size_t)F * F % 64) return fail("Winograd wgrad: F * F must be a multiple of 64");
-    const unsigned rblocks = (unsigned)((size_t)F * F / 64);
+    if ((size_t)F * F % 256) return fail("Winograd wgrad: F * F must be a multiple of 256");
+    const unsigned rblocks = (unsigned)((size_t)F * F / 256);
     tr::wino_wgrad_gemm_kernel<<<dim3(splits, 16), 512, 0, T->st>>>(X, DY, K, WINO_GEMM_ROWS, T->wpart);
-    tr::wino_wgrad_reduce_out_kernel<16><<<rblocks, 1024, 0, T->st>>>(T->wpart, splits, F, g);
+    tr::wino_wgrad_reduce_out_kernel<<<rblocks, 1024, 0, T->st>>>(T->wpart, splits, F, g);
     return hipGetLastError() == hipSuccess ? 0 : fail("Winograd wgrad launch failed");
 }
 
