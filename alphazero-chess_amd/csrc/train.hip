@@ -870,9 +870,12 @@ loss_kernel(const float* __restrict__ logits, const float* __restrict__ tpol, co
 // conv [co][ci][3][3] (burn) -> Wf[t][k][co] (k < kpad, rows >= cin zero) and Wd[t][co][ci] = Wf[8-t]^T
 // ------------------------------------------------------------------ Winograd forward / data grad
 // The 3x3 F -> F convs of the residual tower (F = 256) as Winograd F(2x2, 3x3) -- the inference
-// tower's core (wino.h), 2.25x fewer MFMAs than the implicit GEMM, f32 throughout -- one board
-// per 512-thread workgroup: the board's 64 rows of X into LDS, wino_core, Y (+ addend) back to
-// HBM with no ReLU (BatchNorm runs in training mode after it).  The data grad is the same conv of
+// tower's core (wino.h), 2.25x fewer MFMAs than the implicit GEMM, f32 throughout -- one board at
+// a time per 512-thread workgroup: the board's 64 rows of X into LDS, wino_core, Y (+ addend) back
+// to HBM with no ReLU (BatchNorm runs in training mode after it).  Persistent: AZ_TRAIN_WG
+// workgroups (one per CU) loop over the boards, the weight ring carrying the conv's first steps
+// into the next board (round 5: data-grad convs -2..4 us, bit-identical; the one-board-per-
+// workgroup grid left a re-dispatch gap of up to 5 us per CU between its two boards).  The data grad is the same conv of
 // dY with the flipped, transposed kernel (U built by wino_weights_kernel with flip = 1).
 // STATS: per-board BatchNorm statistics of the output from the epilogue, into part[board][2][F]
 // (the layout of the column-sum partials, one "row block" per board):
@@ -881,6 +884,9 @@ loss_kernel(const float* __restrict__ logits, const float* __restrict__ tpol, co
 //   2 (data grad, the output is the BN backward's dout): sum dz and sum dz * yhat with
 //     dz = dout * (O > 0), yhat = (Ybn - mean) / std -- summed over boards by finalize_bnback_kernel.
 // Either replaces two passes over the 32 MB output (colsum4 + finalize twice, or colsum4<2>).
+#ifndef AZ_TRAIN_WG
+#define AZ_TRAIN_WG 256   // persistent Winograd-conv workgroups: one per CU of MI355X
+#endif
 struct BoardStats {
     float* part;
     const float* O;      // STATS 2: the BN's ReLU output
@@ -917,92 +923,19 @@ template <bool ADD, int STATS, int XIN>
 __global__ void __launch_bounds__(512)
 conv_wino_train_kernel(const float* __restrict__ X, const uint4* __restrict__ U, unsigned ubytes,
                        const float* __restrict__ bias, const float* __restrict__ addend, float* __restrict__ Y,
-                       BoardStats bs, BnIn bn, BnBack bb, unsigned long long* trb) {
+                       BoardStats bs, BnIn bn, BnBack bb, int nboards, unsigned long long* trb) {
     constexpr int F = 256, NN = WinoCfg<F>::NN, XSn = WinoCfg<F>::XS, PF = WinoCfg<F>::PF, RS = F / 4 + 2;
     constexpr int XSZ = 64 * RS, VSZ = 2 * WinoCfg<F>::CH * 1024 / 16, PAD = WINO_PAD_SQ * RS;
     __shared__ __attribute__((aligned(16))) uint4 lds[PAD + XSZ + PAD + VSZ];
     uint4* act = lds + PAD;                              // zero squares either side (wino_core)
     const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const size_t row0 = (size_t)vgpr_index(blockIdx.x) * 64;
-    const uint4* X4 = reinterpret_cast<const uint4*>(X) + row0 * (F / 4);
-    unsigned long long* const tr = trb && w == 0 ? trb + (size_t)vgpr_index(blockIdx.x) * 8 : nullptr;
-    wino_stamp(tr, 0);
-#ifdef AZ_TOWER_TRACE
-    if (tr && lane == 0) {   // where the board ran: HW_ID (CU, SIMD, SE ...) and XCC_ID
-        tr[4] = (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));
-        tr[5] = (unsigned)__builtin_amdgcn_s_getreg(20 | (31 << 11));
-    }
-#endif
-    if constexpr (XIN == 1) {   // thread = channel quad tid % 64 (F / 4 = 64 divides 512) x rows tid / 64 + 8 k
-        static_assert(F / 4 == 64, "BNIN staging assumes 64 channel quads");
-        const int cq = tid & 63;
-        const float4 mu = reinterpret_cast<const float4*>(bn.mean)[cq], sd = reinterpret_cast<const float4*>(bn.stdv)[cq];
-        const float4 ga = reinterpret_cast<const float4*>(bn.gamma)[cq], be = reinterpret_cast<const float4*>(bn.beta)[cq];
-        const float4* R4 = bn.res ? reinterpret_cast<const float4*>(bn.res) + row0 * (F / 4) : nullptr;
-        float4* O4 = reinterpret_cast<float4*>(bn.out) + row0 * (F / 4);
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const int c = tid + 512 * k;
-            const float4 y = reinterpret_cast<const float4*>(X4)[c];
-            float4 v = make_float4(((y.x - mu.x) / sd.x) * ga.x + be.x, ((y.y - mu.y) / sd.y) * ga.y + be.y,
-                                   ((y.z - mu.z) / sd.z) * ga.z + be.z, ((y.w - mu.w) / sd.w) * ga.w + be.w);
-            if (R4) {
-                const float4 q = R4[c];
-                v.x += q.x; v.y += q.y; v.z += q.z; v.w += q.w;
-            }
-            const float4 o = make_float4(fmaxf(v.x, 0.0f), fmaxf(v.y, 0.0f), fmaxf(v.z, 0.0f), fmaxf(v.w, 0.0f));
-            O4[c] = o;
-            act[(c / (F / 4)) * RS + cq] = __builtin_bit_cast(uint4, o);
-        }
-    } else if constexpr (XIN == 2) {   // the same thread layout; X = dout
-        static_assert(F / 4 == 64, "BnBack staging assumes 64 channel quads");
-        const int cq = tid & 63;
-        const float invR = 1.0f / (bb.nglob ? bb.nglob[vgpr_index(0)] : (float)bb.R);   // (a vector load: written by an earlier launch)
-        const float4 mu = reinterpret_cast<const float4*>(bb.mean)[cq], sd = reinterpret_cast<const float4*>(bb.stdv)[cq];
-        const float4 ga = reinterpret_cast<const float4*>(bb.gamma)[cq], dg = reinterpret_cast<const float4*>(bb.dgamma)[cq];
-        const float4 db = reinterpret_cast<const float4*>(bb.dbeta)[cq];
-        const size_t o0 = row0 * (F / 4);
-        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const size_t c = o0 + tid + 512 * k;
-            const float4 d = reinterpret_cast<const float4*>(X)[c], ov = reinterpret_cast<const float4*>(bb.O)[c];
-            const float4 y = reinterpret_cast<const float4*>(bb.Y)[c];
-            const float4 dz = make_float4(ov.x > 0.0f ? d.x : 0.0f, ov.y > 0.0f ? d.y : 0.0f, ov.z > 0.0f ? d.z : 0.0f,
-                                          ov.w > 0.0f ? d.w : 0.0f);
-            const float4 d4 = make_float4((ga.x / sd.x) * (dz.x - db.x * invR - ((y.x - mu.x) / sd.x) * dg.x * invR),
-                                          (ga.y / sd.y) * (dz.y - db.y * invR - ((y.y - mu.y) / sd.y) * dg.y * invR),
-                                          (ga.z / sd.z) * (dz.z - db.z * invR - ((y.z - mu.z) / sd.z) * dg.z * invR),
-                                          (ga.w / sd.w) * (dz.w - db.w * invR - ((y.w - mu.w) / sd.w) * dg.w * invR));
-            reinterpret_cast<float4*>(bb.dy)[c] = d4;
-            if (bb.dres) reinterpret_cast<float4*>(bb.dres)[c] = dz;
-            act[(tid + 512 * k) / (F / 4) * RS + cq] = __builtin_bit_cast(uint4, d4);
-            acc.x += d4.x; acc.y += d4.y; acc.z += d4.z; acc.w += d4.w;
-        }
-        // the board's bias partial: the 8 row phases of each channel quad, in order, through the
-        // (not yet written) V buffers
-        float4* red = reinterpret_cast<float4*>(lds + PAD + XSZ + PAD);
-        red[tid] = acc;
-        __syncthreads();
-        if (tid < 64) {
-            float4 a = red[tid];
-            for (int k = 1; k < 8; k++) {
-                const float4 q = red[64 * k + tid];
-                a.x += q.x; a.y += q.y; a.z += q.z; a.w += q.w;
-            }
-            reinterpret_cast<float4*>(bb.bsum + (size_t)vgpr_index(blockIdx.x) * 2 * F)[tid] = a;   // [board][2][F]
-        }
-    } else {
-        for (int c = tid; c < 64 * (F / 4); c += 512) act[(c / (F / 4)) * RS + c % (F / 4)] = X4[c];
-    }
     for (int c = tid; c < PAD; c += 512) {
         lds[c] = make_uint4(0, 0, 0, 0);
         act[XSZ + c] = make_uint4(0, 0, 0, 0);
     }
-    __syncthreads();   // (XIN 2: also orders the bias partial's reads of V before wino_core writes V)
-    wino_stamp(tr, 1);
+    // persistent: the workgroup loops over boards blockIdx.x, + gridDim.x, ...; the weight ring's
+    // refills past the conv's last step read its first steps again (rN = rW), for the next board
     const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc((void*)U, (short)0, (int)ubytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rN = __builtin_amdgcn_make_buffer_rsrc((void*)U, (short)0, 0, 0x00020000);
     const int voff = wino_voff<F>(w, lane);
     f32x4 wr[PF][XSn][NN];
 #pragma unroll
@@ -1013,63 +946,141 @@ conv_wino_train_kernel(const float* __restrict__ X, const uint4* __restrict__ U,
             for (int n = 0; n < NN; n++)
                 wr[i][xs][n] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                                              rW, voff + n * 1024 + wino_toff<F>(0, i * XSn + xs), 0, 0));
-    f32x4 y[NN][4];
-    wino_core<F>(reinterpret_cast<char*>(act), (XSZ + PAD) * 16, rW, rN, bias, wr, w, lane, y);
-    wino_stamp(tr, 2);
-    const int l16 = lane & 15, h = lane >> 4, ty = l16 >> 2, tx = l16 & 3;
-    const int co0 = w * 16 * NN + h * 4;
-    f32x4 s0[NN], s1[NN];
-#pragma unroll
-    for (int n = 0; n < NN; n++) {
-        s0[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-        s1[n] = s0[n];
-        f32x4 mu = s0[n], sd = s0[n];
-        if constexpr (STATS == 2) {
-            mu = *reinterpret_cast<const f32x4*>(bs.mean + co0 + n * 16);
-            sd = *reinterpret_cast<const f32x4*>(bs.stdv + co0 + n * 16);
+#pragma unroll 1
+    for (int bid = blockIdx.x; bid < nboards; bid += gridDim.x) {
+        const size_t row0 = (size_t)vgpr_index(bid) * 64;
+        const uint4* X4 = reinterpret_cast<const uint4*>(X) + row0 * (F / 4);
+        unsigned long long* const tr = trb && w == 0 ? trb + (size_t)vgpr_index(bid) * 8 : nullptr;
+        wino_stamp(tr, 0);
+#ifdef AZ_TOWER_TRACE
+        if (tr && lane == 0) {   // where the board ran: HW_ID (CU, SIMD, SE ...) and XCC_ID
+            tr[4] = (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));
+            tr[5] = (unsigned)__builtin_amdgcn_s_getreg(20 | (31 << 11));
         }
+#endif
+        if constexpr (XIN == 1) {   // thread = channel quad tid % 64 (F / 4 = 64 divides 512) x rows tid / 64 + 8 k
+            static_assert(F / 4 == 64, "BNIN staging assumes 64 channel quads");
+            const int cq = tid & 63;
+            const float4 mu = reinterpret_cast<const float4*>(bn.mean)[cq], sd = reinterpret_cast<const float4*>(bn.stdv)[cq];
+            const float4 ga = reinterpret_cast<const float4*>(bn.gamma)[cq], be = reinterpret_cast<const float4*>(bn.beta)[cq];
+            const float4* R4 = bn.res ? reinterpret_cast<const float4*>(bn.res) + row0 * (F / 4) : nullptr;
+            float4* O4 = reinterpret_cast<float4*>(bn.out) + row0 * (F / 4);
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const size_t o = (row0 + (2 * ty + (q >> 1)) * 8 + 2 * tx + (q & 1)) * F + co0 + n * 16;
-            f32x4 v = y[n][q];
-            if constexpr (ADD) v += *reinterpret_cast<const f32x4*>(addend + o);
-            *reinterpret_cast<f32x4*>(Y + o) = v;
-            if constexpr (STATS == 1) {
-                y[n][q] = v;
-                s0[n] += v;
-            } else if constexpr (STATS == 2) {
-                const f32x4 ov = *reinterpret_cast<const f32x4*>(bs.O + o);
-                const f32x4 yb = *reinterpret_cast<const f32x4*>(bs.Ybn + o);
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const float dz = ov[r] > 0.0f ? v[r] : 0.0f;
-                    s0[n][r] += dz;
-                    s1[n][r] += dz * ((yb[r] - mu[r]) / sd[r]);
+            for (int k = 0; k < 8; k++) {
+                const int c = tid + 512 * k;
+                const float4 y = reinterpret_cast<const float4*>(X4)[c];
+                float4 v = make_float4(((y.x - mu.x) / sd.x) * ga.x + be.x, ((y.y - mu.y) / sd.y) * ga.y + be.y,
+                                       ((y.z - mu.z) / sd.z) * ga.z + be.z, ((y.w - mu.w) / sd.w) * ga.w + be.w);
+                if (R4) {
+                    const float4 q = R4[c];
+                    v.x += q.x; v.y += q.y; v.z += q.z; v.w += q.w;
                 }
+                const float4 o = make_float4(fmaxf(v.x, 0.0f), fmaxf(v.y, 0.0f), fmaxf(v.z, 0.0f), fmaxf(v.w, 0.0f));
+                O4[c] = o;
+                act[(c / (F / 4)) * RS + cq] = __builtin_bit_cast(uint4, o);
             }
+        } else if constexpr (XIN == 2) {   // the same thread layout; X = dout
+            static_assert(F / 4 == 64, "BnBack staging assumes 64 channel quads");
+            const int cq = tid & 63;
+            const float invR = 1.0f / (bb.nglob ? bb.nglob[vgpr_index(0)] : (float)bb.R);   // (a vector load: written by an earlier launch)
+            const float4 mu = reinterpret_cast<const float4*>(bb.mean)[cq], sd = reinterpret_cast<const float4*>(bb.stdv)[cq];
+            const float4 ga = reinterpret_cast<const float4*>(bb.gamma)[cq], dg = reinterpret_cast<const float4*>(bb.dgamma)[cq];
+            const float4 db = reinterpret_cast<const float4*>(bb.dbeta)[cq];
+            const size_t o0 = row0 * (F / 4);
+            float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const size_t c = o0 + tid + 512 * k;
+                const float4 d = reinterpret_cast<const float4*>(X)[c], ov = reinterpret_cast<const float4*>(bb.O)[c];
+                const float4 y = reinterpret_cast<const float4*>(bb.Y)[c];
+                const float4 dz = make_float4(ov.x > 0.0f ? d.x : 0.0f, ov.y > 0.0f ? d.y : 0.0f, ov.z > 0.0f ? d.z : 0.0f,
+                                              ov.w > 0.0f ? d.w : 0.0f);
+                const float4 d4 = make_float4((ga.x / sd.x) * (dz.x - db.x * invR - ((y.x - mu.x) / sd.x) * dg.x * invR),
+                                              (ga.y / sd.y) * (dz.y - db.y * invR - ((y.y - mu.y) / sd.y) * dg.y * invR),
+                                              (ga.z / sd.z) * (dz.z - db.z * invR - ((y.z - mu.z) / sd.z) * dg.z * invR),
+                                              (ga.w / sd.w) * (dz.w - db.w * invR - ((y.w - mu.w) / sd.w) * dg.w * invR));
+                reinterpret_cast<float4*>(bb.dy)[c] = d4;
+                if (bb.dres) reinterpret_cast<float4*>(bb.dres)[c] = dz;
+                act[(tid + 512 * k) / (F / 4) * RS + cq] = __builtin_bit_cast(uint4, d4);
+                acc.x += d4.x; acc.y += d4.y; acc.z += d4.z; acc.w += d4.w;
+            }
+            // the board's bias partial: the 8 row phases of each channel quad, in order, through the
+            // (not yet written) V buffers
+            float4* red = reinterpret_cast<float4*>(lds + PAD + XSZ + PAD);
+            red[tid] = acc;
+            __syncthreads();
+            if (tid < 64) {
+                float4 a = red[tid];
+                for (int k = 1; k < 8; k++) {
+                    const float4 q = red[64 * k + tid];
+                    a.x += q.x; a.y += q.y; a.z += q.z; a.w += q.w;
+                }
+                reinterpret_cast<float4*>(bb.bsum + (size_t)vgpr_index(bid) * 2 * F)[tid] = a;   // [board][2][F]
+            }
+        } else {
+            for (int c = tid; c < 64 * (F / 4); c += 512) act[(c / (F / 4)) * RS + c % (F / 4)] = X4[c];
         }
-    }
-    if constexpr (STATS != 0) {
+        __syncthreads();   // (XIN 2: also orders the bias partial's reads of V before wino_core writes V)
+        wino_stamp(tr, 1);
+        f32x4 y[NN][4];
+        wino_core<F>(reinterpret_cast<char*>(act), (XSZ + PAD) * 16, rW, rW, bias, wr, w, lane, y);
+        wino_stamp(tr, 2);
+        const int l16 = lane & 15, h = lane >> 4, ty = l16 >> 2, tx = l16 & 3;
+        const int co0 = w * 16 * NN + h * 4;
+        f32x4 s0[NN], s1[NN];
 #pragma unroll
         for (int n = 0; n < NN; n++) {
-            s0[n] = sum16(s0[n]);
-            if constexpr (STATS == 1) {
-                const f32x4 mb = s0[n] / 64.0f;   // the board's mean (64 squares)
+            s0[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+            s1[n] = s0[n];
+            f32x4 mu = s0[n], sd = s0[n];
+            if constexpr (STATS == 2) {
+                mu = *reinterpret_cast<const f32x4*>(bs.mean + co0 + n * 16);
+                sd = *reinterpret_cast<const f32x4*>(bs.stdv + co0 + n * 16);
+            }
 #pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const f32x4 d = y[n][q] - mb;
-                    s1[n] += d * d;
+            for (int q = 0; q < 4; q++) {
+                const size_t o = (row0 + (2 * ty + (q >> 1)) * 8 + 2 * tx + (q & 1)) * F + co0 + n * 16;
+                f32x4 v = y[n][q];
+                if constexpr (ADD) v += *reinterpret_cast<const f32x4*>(addend + o);
+                *reinterpret_cast<f32x4*>(Y + o) = v;
+                if constexpr (STATS == 1) {
+                    y[n][q] = v;
+                    s0[n] += v;
+                } else if constexpr (STATS == 2) {
+                    const f32x4 ov = *reinterpret_cast<const f32x4*>(bs.O + o);
+                    const f32x4 yb = *reinterpret_cast<const f32x4*>(bs.Ybn + o);
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const float dz = ov[r] > 0.0f ? v[r] : 0.0f;
+                        s0[n][r] += dz;
+                        s1[n][r] += dz * ((yb[r] - mu[r]) / sd[r]);
+                    }
                 }
             }
-            s1[n] = sum16(s1[n]);
-            if (l16 == 0) {
-                float* pb = bs.part + (size_t)vgpr_index(blockIdx.x) * 2 * F + co0 + n * 16;
-                *reinterpret_cast<f32x4*>(pb) = s0[n];
-                *reinterpret_cast<f32x4*>(pb + F) = s1[n];
+        }
+        if constexpr (STATS != 0) {
+#pragma unroll
+            for (int n = 0; n < NN; n++) {
+                s0[n] = sum16(s0[n]);
+                if constexpr (STATS == 1) {
+                    const f32x4 mb = s0[n] / 64.0f;   // the board's mean (64 squares)
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const f32x4 d = y[n][q] - mb;
+                        s1[n] += d * d;
+                    }
+                }
+                s1[n] = sum16(s1[n]);
+                if (l16 == 0) {
+                    float* pb = bs.part + (size_t)vgpr_index(bid) * 2 * F + co0 + n * 16;
+                    *reinterpret_cast<f32x4*>(pb) = s0[n];
+                    *reinterpret_cast<f32x4*>(pb + F) = s1[n];
+                }
             }
         }
+        wino_stamp(tr, 3);
+        __syncthreads();   // every wave is done with ACT and V before the next board's staging
     }
-    wino_stamp(tr, 3);
 }
 
 // Winograd weights U = G g G^T (f64, rounded once to f32: the same arithmetic as net.hip's
@@ -1367,22 +1378,23 @@ int launch_wino(Trainer* T, const float* X, const float* U, const float* bias, c
         trb = g_trace + (size_t)(g_trace_n++ % TRACE_LAUNCHES) * TRACE_BOARDS * 8;
     }
 #endif
+    const unsigned wg = (unsigned)std::min(B, AZ_TRAIN_WG);   // persistent workgroups (one per CU)
     if (bn.out)
-        tr::conv_wino_train_kernel<false, 1, 1><<<B, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, trb);
+        tr::conv_wino_train_kernel<false, 1, 1><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb);
     else if (bb.dy && addend)
-        tr::conv_wino_train_kernel<true, 2, 2><<<B, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, trb);
+        tr::conv_wino_train_kernel<true, 2, 2><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, trb);
     else if (bb.dy)
-        tr::conv_wino_train_kernel<false, 2, 2><<<B, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, trb);
+        tr::conv_wino_train_kernel<false, 2, 2><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb);
     else if (addend && stats == 2)
-        tr::conv_wino_train_kernel<true, 2, 0><<<B, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, trb);
+        tr::conv_wino_train_kernel<true, 2, 0><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, trb);
     else if (addend && stats == 0)
-        tr::conv_wino_train_kernel<true, 0, 0><<<B, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, trb);
+        tr::conv_wino_train_kernel<true, 0, 0><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, trb);
     else if (!addend && stats == 1)
-        tr::conv_wino_train_kernel<false, 1, 0><<<B, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, trb);
+        tr::conv_wino_train_kernel<false, 1, 0><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb);
     else if (!addend && stats == 2)
-        tr::conv_wino_train_kernel<false, 2, 0><<<B, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, trb);
+        tr::conv_wino_train_kernel<false, 2, 0><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb);
     else if (!addend && stats == 0)
-        tr::conv_wino_train_kernel<false, 0, 0><<<B, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, trb);
+        tr::conv_wino_train_kernel<false, 0, 0><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb);
     else
         return fail("Winograd conv: unsupported statistics mode");
     return hipGetLastError() == hipSuccess ? 0 : fail("Winograd conv launch failed");
