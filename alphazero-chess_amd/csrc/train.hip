@@ -1094,28 +1094,47 @@ __global__ void __launch_bounds__(256) wino_weights_kernel(const float* __restri
     const int idx = blockIdx.x * blockDim.x + threadIdx.x, flip = blockIdx.y & 1;
     const float* __restrict__ w = w0 + (blockIdx.y >> 1) * wstride;
     float* __restrict__ U = U0 + (size_t)blockIdx.y * ustride;
-    if (idx >= F * F) return;
-    // thread -> (output o, input i) in the order of U's innermost dimensions (i % 4, o % 16,
-    // (i % 16) / 4), so that a workgroup's stores of one point are 1 KB contiguous (o = idx / F,
-    // i = idx % F wrote 16-byte pieces 256 B apart: 309 us for the step's 80 transforms); a
-    // workgroup covers a 16 x 16 (o, i) block, whose weight reads are rows of 16 x 9 floats
-    const int blk = idx >> 8, o = (blk % (F / 16)) * 16 + ((idx >> 2) & 15);
-    const int i = (blk / (F / 16)) * 16 + ((idx >> 6) & 3) * 4 + (idx & 3);   // output / input channel of U's conv
-    double g[3][3];
-    for (int ky = 0; ky < 3; ky++)
-        for (int kx = 0; kx < 3; kx++)
-            g[ky][kx] = flip ? (double)w[((size_t)i * F + o) * 9 + (2 - ky) * 3 + (2 - kx)]
-                             : (double)w[((size_t)o * F + i) * 9 + ky * 3 + kx];
+    if (idx >= F * F / 4) return;
+    // thread -> (output o, four inputs i0 .. i0 + 3): U's innermost dimension is i % 4, so each
+    // point is one 16-byte store, and a wave's 64 lanes -- (o % 16, (i % 16) / 4) of one 16 x 16
+    // (o, i) block -- write 1 KB contiguous per point.  (Round 5: one i per thread with four-byte
+    // stores: 145 us for the step's 80 transforms; this form 134 us, bit-identical.)  The arithmetic
+    // per element is unchanged (f64, rounded once).
+    const int l = idx & 63, wv = idx >> 6, CF = F / 16;
+    const int o = (wv % CF) * 16 + (l & 15), i0 = (wv / CF) * 16 + (l >> 4) * 4;
+    float gf[4][9];   // [i - i0][ky 3 + kx] of U's conv
+    if (!flip) {      // the four kernels are 36 consecutive floats, 16-byte aligned
+        const float4* src = reinterpret_cast<const float4*>(w + ((size_t)o * F + i0) * 9);
+#pragma unroll
+        for (int q = 0; q < 9; q++) {
+            const float4 t = src[q];
+            gf[(4 * q) / 9][(4 * q) % 9] = t.x;
+            gf[(4 * q + 1) / 9][(4 * q + 1) % 9] = t.y;
+            gf[(4 * q + 2) / 9][(4 * q + 2) % 9] = t.z;
+            gf[(4 * q + 3) / 9][(4 * q + 3) % 9] = t.w;
+        }
+    } else {          // the data grad's flipped, transposed kernel
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+#pragma unroll
+            for (int t = 0; t < 9; t++) gf[j][t] = w[((size_t)(i0 + j) * F + o) * 9 + 8 - t];
+    }
     const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
-    const int CF = F / 16;
+#pragma unroll
     for (int a = 0; a < 4; a++) {
-        double gg[3];
-        for (int j = 0; j < 3; j++) gg[j] = G[a][0] * g[0][j] + G[a][1] * g[1][j] + G[a][2] * g[2][j];
+        double gg[4][3];
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+#pragma unroll
+            for (int c = 0; c < 3; c++)
+                gg[j][c] = G[a][0] * (double)gf[j][c] + G[a][1] * (double)gf[j][3 + c] + G[a][2] * (double)gf[j][6 + c];
+#pragma unroll
         for (int b = 0; b < 4; b++) {
-            const double u = gg[0] * G[b][0] + gg[1] * G[b][1] + gg[2] * G[b][2];
-            const int step = (i / 16) * 16 + a * 4 + b;
-            const int lane = (o % 16) + 16 * ((i % 16) / 4);
-            U[(((size_t)step * CF + o / 16) * 64 + lane) * 4 + i % 4] = (float)u;
+            float u[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) u[j] = (float)(gg[j][0] * G[b][0] + gg[j][1] * G[b][1] + gg[j][2] * G[b][2]);
+            const int step = (i0 / 16) * 16 + a * 4 + b;
+            *reinterpret_cast<float4*>(U + (((size_t)step * CF + o / 16) * 64 + l) * 4) = make_float4(u[0], u[1], u[2], u[3]);
         }
     }
 }
@@ -1649,7 +1668,7 @@ int trainer_grads(Trainer* T, const float* planes, const float* tpol, const floa
     if (T->wino && T->blocks > 0) {  // residual convs: Winograd weights, forward and data grad, one launch
         const size_t wstride = L.tower.size() > 2 ? L.tower[2].w - L.tower[1].w : 0;
         if (F % 16) return fail("train: Winograd weights need F % 16 == 0");
-        tr::wino_weights_kernel<<<dim3((unsigned)((F * F + 255) / 256), 2 * (L.tower.size() - 1)), 256, 0, st>>>(
+        tr::wino_weights_kernel<<<dim3((unsigned)((F * F / 4 + 255) / 256), 2 * (L.tower.size() - 1)), 256, 0, st>>>(
             T->p + L.tower[1].w, wstride, F, T->ubase, T->ubytes / sizeof(float));
     }
     for (size_t i = 0; i < L.tower.size(); i++) {
