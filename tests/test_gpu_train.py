@@ -236,6 +236,40 @@ def test_winograd_training_convs_match_direct(require_gpu, monkeypatch):
         assert np.linalg.norm(g1[o:o + cnt] - r) <= 1e-2 * max(np.linalg.norm(r), 1e-30), name
 
 
+@pytest.mark.parametrize("blocks,n", [(2, 300), (3, 13)])
+def test_bn_staging_matches_separate_bn_kernels(require_gpu, monkeypatch, blocks, n):
+    """The BatchNorm apply / backward staged in the Winograd convs (the default) against the same
+    step with separate BN kernels (AZ_TRAIN_FUSE_BN=0: bn_apply4 / bn_back4 and the convs' plain
+    staging): the staging does their arithmetic element for element and both take the statistics
+    from the convs' per-board partials, so losses, running statistics and every gradient but the
+    BN-fed conv biases are bit-identical (those biases' exact gradient is 0: their partial sums
+    are added in another order, |g| <= 1e-5 either way).  n = 300 boards: the persistent convs'
+    256 workgroups take two boards each for 44 of them; n = 13: fewer boards than workgroups."""
+    w = A.random_weights(blocks, 256, seed=23)
+    planes, tpol, tval = batch(n, seed=400 + n)
+    out = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("AZ_TRAIN_FUSE_BN", flag)
+        tr = A.Trainer(blocks, 256, weights=w, max_batch=n)
+        losses = tr.compute_gradients(planes, tpol, tval)
+        out[flag] = (losses, tr.grads(), tr.params())
+    (l1, g1, p1), (l0, g0, p0) = out["1"], out["0"]
+    assert l1 == l0
+    assert np.array_equal(p1, p0)                 # running statistics
+    seg, _ = T.segments(blocks, 256)
+    zero_bias = bn_fed_biases(blocks)
+    checked = 0
+    for name, (o, shape, bn) in seg.items():
+        cnt = 2 * shape[1] if bn else int(np.prod(shape))
+        a, b = g1[o:o + cnt], g0[o:o + cnt]
+        if name in zero_bias:
+            assert np.abs(a).max() <= 1e-5 and np.abs(b).max() <= 1e-5, name
+            continue
+        assert np.array_equal(a, b), (name, np.abs(a - b).max())
+        checked += 1
+    assert checked > 4 * blocks
+
+
 def test_winograd_weight_grad_multi_split(require_gpu):
     """the production Winograd weight grad (wino_wgrad_gemm_kernel, 512 rows of
     (board, tile) per split, the splits summed by wino_wgrad_reduce_out_kernel) with more than one
