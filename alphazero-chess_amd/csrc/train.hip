@@ -162,7 +162,9 @@ constexpr int GK = 64, GN = 64, GR = 64, GS = 80;
 
 // NB independent problems (X + i xbs, DY + i dbs: the 16 Winograd points of a weight grad) share
 // one launch: blockIdx.z = problem * splits + split, partial[split][problem][t][k][n].
-template <int TAPS>
+// KI: the 16-channel k blocks of the tile that hold data (4; 2 for the input conv's 32 padded
+// channels, whose upper half would only multiply zeros)
+template <int TAPS, int KI = 4>
 __global__ void __launch_bounds__(256)
 wgrad_f32_kernel(const float* __restrict__ X, int ldx, int K, const float* __restrict__ DY, int ldd, int N, int R,
                  int rows_per_split, float* __restrict__ partial, int nb, size_t xbs, size_t dbs) {
@@ -174,11 +176,11 @@ wgrad_f32_kernel(const float* __restrict__ X, int ldx, int K, const float* __res
     X += pb * xbs;
     DY += pb * dbs;
     const int rbeg = split * rows_per_split, rend = min(R, rbeg + rows_per_split);
-    f32x4 acc[TAPS][4];
+    f32x4 acc[TAPS][KI];
 #pragma unroll
     for (int t = 0; t < TAPS; t++)
 #pragma unroll
-        for (int i = 0; i < 4; i++) acc[t][i] = f32x4{0, 0, 0, 0};
+        for (int i = 0; i < KI; i++) acc[t][i] = f32x4{0, 0, 0, 0};
     if (tid < GS) xs[GR * GS + tid] = 0.0f;
     // software pipeline: the next GR rows of X and dY are read into registers while the current
     // rows' MFMAs run, and written to LDS after the barrier
@@ -190,7 +192,7 @@ wgrad_f32_kernel(const float* __restrict__ X, int ldx, int K, const float* __res
             const int i = tid + j * 256, rr = i >> 4, c4 = (i & 15) * 4;
             xv[j] = dv[j] = make_float4(0.f, 0.f, 0.f, 0.f);
             if (rc + rr < rend) {
-                if (k0 + c4 < K) xv[j] = *reinterpret_cast<const float4*>(X + (size_t)(rc + rr) * ldx + k0 + c4);
+                if (c4 < 16 * KI && k0 + c4 < K) xv[j] = *reinterpret_cast<const float4*>(X + (size_t)(rc + rr) * ldx + k0 + c4);
                 if (n0 + c4 < N) dv[j] = *reinterpret_cast<const float4*>(DY + (size_t)(rc + rr) * ldd + n0 + c4);
             }
         }
@@ -217,7 +219,7 @@ wgrad_f32_kernel(const float* __restrict__ X, int ldx, int K, const float* __res
                 if constexpr (TAPS == 9) ok = tap_src(rq, t, src);
                 const int base = ok ? src * GS : GR * GS;
 #pragma unroll
-                for (int i = 0; i < 4; i++)
+                for (int i = 0; i < KI; i++)
                     acc[t][i] = __builtin_amdgcn_mfma_f32_16x16x4f32(xs[base + i * 16 + (lane & 15)], b, acc[t][i], 0, 0, 0);
             }
         }
@@ -227,7 +229,7 @@ wgrad_f32_kernel(const float* __restrict__ X, int ldx, int K, const float* __res
 #pragma unroll
     for (int t = 0; t < TAPS; t++)
 #pragma unroll
-        for (int i = 0; i < 4; i++)
+        for (int i = 0; i < KI; i++)
 #pragma unroll
             for (int g = 0; g < 4; g++) {
                 const int kd = k0 + i * 16 + (lane >> 4) * 4 + g;
@@ -1435,7 +1437,9 @@ int launch_wgrad(Trainer* T, int taps, const float* X, int ldx, int K, const flo
     const int rps = wgrad_rows_per_split(taps, R);
     const int splits = (int)wgrad_splits(taps, R);
     dim3 grid((K + tr::GK - 1) / tr::GK, (N + tr::GN - 1) / tr::GN, splits);
-    if (taps == 9) tr::wgrad_f32_kernel<9><<<grid, 256, 0, T->st>>>(X, ldx, K, DY, ldd, N, R, rps, T->wpart, 1, 0, 0);
+    if (taps == 9 && K <= 32)   // the input conv (32 padded channels): half the k tile
+        tr::wgrad_f32_kernel<9, 2><<<grid, 256, 0, T->st>>>(X, ldx, K, DY, ldd, N, R, rps, T->wpart, 1, 0, 0);
+    else if (taps == 9) tr::wgrad_f32_kernel<9><<<grid, 256, 0, T->st>>>(X, ldx, K, DY, ldd, N, R, rps, T->wpart, 1, 0, 0);
     else tr::wgrad_f32_kernel<1><<<grid, 256, 0, T->st>>>(X, ldx, K, DY, ldd, N, R, rps, T->wpart, 1, 0, 0);
     const size_t n = (size_t)taps * K * N;
     tr::reduce_kernel<<<grid_for(n), 256, 0, T->st>>>(T->wpart, splits, n, out);
