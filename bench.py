@@ -418,7 +418,7 @@ def main():
     ap.add_argument("--cpu-sims", type=int, default=32, help="sims per sampled search (batched leg ~10 s of host work at 20x256)")
     ap.add_argument("--train-steps", type=int, default=5, help="timed training steps (0 = skip the training phase)")
     ap.add_argument("--train-batch", type=int, default=512, help="positions per rank (BATCH_SIZE, parameters.rs:17)")
-    ap.add_argument("--train-timeout", type=int, default=240)
+    ap.add_argument("--train-timeout", type=int, default=90)
     ap.add_argument("--train-mode", default="per-rank", choices=["per-rank", "sharded"], help=argparse.SUPPRESS)
     ap.add_argument("--games-leg", type=int, default=1,
                     help="1: also play C2's games (256 x 800 sims, 6x64 f32) from startpos to the end on every rank "
