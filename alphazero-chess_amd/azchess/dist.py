@@ -31,6 +31,29 @@ def reduce_run(elapsed, counters, world, device=None):
     return float(t.item()), [float(v) for v in c.tolist()]
 
 
+def allgather_bytes(payload, group=None):
+    """Every rank's byte string, in rank order, over the initialised torch.distributed group (gloo:
+    host tensors; nccl: tensors on the current device).  Used once per self-play pass to replicate
+    the replay buffer (memory.add_from_ranks), never on the search path."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    dev = torch.device("cpu")
+    if dist.get_backend(group) != "gloo":
+        dev = torch.device("cuda", torch.cuda.current_device())
+    n = torch.tensor([len(payload)], dtype=torch.int64, device=dev)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    sizes = [int(s.item()) for s in sizes]
+    m = max(max(sizes), 1)
+    buf = torch.zeros(m, dtype=torch.uint8, device=dev)
+    if payload:
+        buf[:len(payload)] = torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(dev)
+    outs = [torch.empty(m, dtype=torch.uint8, device=dev) for _ in range(world)]
+    dist.all_gather(outs, buf, group=group)
+    return [o[:s].cpu().numpy().tobytes() for o, s in zip(outs, sizes)]
+
+
 def barrier(world):
     if world > 1:
         import torch.distributed as dist

@@ -247,6 +247,13 @@ class Trainer:
         L.check(L.lib.az_trainer_timing(self._h, C.byref(a), C.byref(b), C.byref(n), int(reset)))
         return a.value, b.value, n.value
 
+    def exchange_stats(self, reset=False):
+        """(collectives, steps, exchange_ms): the data-parallel exchanges since the last reset --
+        how many, over how many applied steps, and their device time."""
+        a, b, c = C.c_int64(), C.c_int64(), C.c_double()
+        L.check(L.lib.az_trainer_exchange_stats(self._h, C.byref(a), C.byref(b), C.byref(c), int(reset)))
+        return a.value, b.value, c.value
+
     def model(self, dtype="f32"):
         """model.valid() for self-play (training.rs:83): an inference net with the current weights,
         f32 like the reference's Cuda<f32> backend (bf16 is an explicit throughput opt-in)."""
@@ -254,74 +261,130 @@ class Trainer:
         return AlphaZero(self.blocks, self.filters, weights=self.params(), dtype=dtype, device=self.device)
 
 
+def sample_seed(seed, iteration, step, rank=None):
+    """Seed of one training step's replay sample.  rank None: the seed every rank shares (one global
+    batch drawn from the replicated buffer); else a per-rank stream."""
+    s = (seed << 20) ^ (iteration << 8) ^ step
+    return s if rank is None else s ^ rank << 40
+
+
+def shard_bounds(n, rank, world):
+    """This rank's contiguous rows [lo, hi) of an n-row global batch."""
+    return rank * n // world, (rank + 1) * n // world
+
+
+def _default_allgather():
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        raise ValueError("train: world > 1 with a shared replay buffer needs allgather= or an initialised "
+                         "torch.distributed group")
+    from .dist import allgather_bytes
+    return allgather_bytes
+
+
 def train(iterations, blocks=NUM_RES_BLOCKS, filters=NUM_FILTERS, games=NUM_EPISODES, sims=NUM_SIMULATIONS,
           min_replay=MIN_REPLAY_SIZE, train_steps=NUM_TRAIN_STEPS, batch_size=BATCH_SIZE, replay=None, trainer=None,
-          device=0, seed=SEED, dtype="f32", comm=None, shard_batch=False, reducer=None, log=None):
+          device=0, seed=SEED, dtype="f32", comm=None, shard_batch=None, reducer=None, shared_replay=None,
+          allgather=None, log=None, log_batch=None):
     """train() (training.rs:39-275) without the TUI, arena and Elo (SKIP_VALIDATION = true,
     parameters.rs:35): per iteration, self-play `games` games with model.valid() until the replay
     buffer holds min_replay unique positions, then train_steps AdamW steps on batches of
     batch_size at get_cyclical_lr(iteration); the new model replaces the old one.
-    comm = (unique_id, rank, world) makes the gradient step data-parallel over RCCL: every rank
-    plays its own games (seed offset by rank) into its own buffer.  shard_batch (with comm): each
-    step is the reference's ONE batch of batch_size split over the ranks (batch_size / world per
-    rank, az_trainer_set_sharded: BatchNorm statistics over the whole batch); without it every
-    rank trains its own batch_size (global batch batch_size x world, per-rank BatchNorm).
-    reducer = (reduce, rank, world) instead of comm: the same exchanges through a host callback
-    (Trainer.set_host_reducer; e.g. gloo, or ranks as threads of one process).
-    Returns (trainer, replay, per-iteration stats)."""
-    from .memory import ReplayBuffer
+
+    Data parallel (comm = (unique_id, rank, world) over RCCL, or reducer = (reduce, rank, world)
+    through a host callback, Trainer.set_host_reducer): every rank plays its own games (seed offset
+    by rank), and by default (world > 1) the loop computes the reference's train() itself:
+      * shared_replay (default on): ONE replay buffer (memory.rs:41-96), replicated -- after each
+        self-play pass the ranks exchange their drained EpisodeSteps through allgather(bytes) ->
+        [bytes per rank] (default: azchess.dist.allgather_bytes over torch.distributed) and every
+        rank adds the union in (rank, drain) order (memory.add_from_ranks), so MIN_REPLAY_SIZE is
+        tested on the global length and every rank leaves self-play together;
+      * shard_batch (default on): each step is the reference's ONE batch of batch_size
+        (training.rs:137-138), drawn with a seed shared by all ranks, and each rank trains its
+        contiguous slice (az_trainer_set_sharded: BatchNorm statistics, BN backward and the loss
+        over the whole batch).
+    Labelled opt-ins: shard_batch=False trains batch_size per rank (global batch batch_size x world,
+    per-rank BatchNorm, averaged gradients); shared_replay=False keeps one buffer per rank.
+    log_batch(iteration, step, planes, policy, value, lo, hi): each step's drawn batch and this
+    rank's rows of it.  Returns (trainer, replay, per-iteration stats)."""
+    from .memory import ReplayBuffer, add_from_ranks
     if comm and reducer:
         raise ValueError("train: comm (RCCL) or reducer (host), not both")
     rank, world = (comm[1], comm[2]) if comm else (reducer[1], reducer[2]) if reducer else (0, 1)
-    if shard_batch and batch_size % world:
-        raise ValueError("shard_batch: batch_size %d is not a multiple of world %d" % (batch_size, world))
-    local_batch = batch_size // world if shard_batch else batch_size
+    shard_batch = world > 1 if shard_batch is None else bool(shard_batch)
+    shared_replay = world > 1 if shared_replay is None else bool(shared_replay)
+    if shard_batch and batch_size < world:
+        raise ValueError("shard_batch: batch_size %d is smaller than world %d" % (batch_size, world))
+    if shared_replay and world > 1 and allgather is None:
+        allgather = _default_allgather()
+    # the largest shard a rank can get of a (possibly short) global batch
+    local_batch = -(-batch_size // world) if shard_batch else batch_size
     if trainer is None:
         trainer = Trainer(blocks, filters, max_batch=local_batch, device=device, seed=seed)
         if comm:
             trainer.set_comm(*comm)
         elif reducer:
             trainer.set_host_reducer(*reducer)
-        if shard_batch:
-            trainer.set_sharded(True)
+    trainer.set_sharded(shard_batch)   # a caller's trainer too (its comm / reducer is the caller's)
     replay = replay if replay is not None else ReplayBuffer()
     history = []
     for iteration in range(iterations):
         t0 = time.perf_counter()
         model = trainer.model(dtype)
         new_unique, plays, sims_done, games_done, steps_done, moves_done, finished = 0, 0, 0, 0, 0, 0, 0
+        steps_global = 0
         while True:
             sp = SelfPlay(model, games=games, sims=sims, device=device, continuous=False,
                           seed=seed + 1000003 * rank + 7919 * iteration + 104729 * plays)
             sp.reset()
+            local = []
             while True:
                 _, active = sp.step()
-                for st in sp.drain_raw():
-                    new_unique += replay.add(st)
-                    steps_done += 1
+                drained = sp.drain_raw()
+                steps_done += len(drained)
+                if shared_replay and world > 1:
+                    local += drained
+                else:
+                    new_unique += replay.add_many(drained)
                 if active == 0:
                     break
+            if shared_replay and world > 1:
+                nu, added = add_from_ranks(replay, local, allgather)
+                new_unique += nu
+                steps_global += added
             plays += 1
             ss = sp.search.stats()
             sims_done += ss["sims"]
             moves_done += ss["moves"]
             finished += ss["games_finished"]
             games_done += games
-            if len(replay) >= min_replay:
+            if len(replay) >= min_replay:   # the global length when the buffer is shared
                 break
         t1 = time.perf_counter()
         lr = get_cyclical_lr(iteration)
         pl_sum = vl_sum = 0.0
         for b in range(train_steps):
-            planes, pol, val, _ = replay.sample_arrays(local_batch, seed=(seed << 20) ^ (iteration << 8) ^ b ^ rank << 40)
-            pl, vl = trainer.step(planes, pol, val, lr)
+            if shared_replay and shard_batch:     # one global batch, this rank's slice
+                planes, pol, val, _ = replay.sample_arrays(batch_size, seed=sample_seed(seed, iteration, b))
+                lo, hi = shard_bounds(planes.shape[0], rank, world)
+                if hi <= lo:
+                    raise ValueError("train: a %d-position batch leaves rank %d no rows" % (planes.shape[0], rank))
+            else:
+                n = -(-batch_size // world) if shard_batch else batch_size
+                planes, pol, val, _ = replay.sample_arrays(n, seed=sample_seed(seed, iteration, b, rank))
+                lo, hi = 0, planes.shape[0]
+            if log_batch:
+                log_batch(iteration, b, planes, pol, val, lo, hi)
+            pl, vl = trainer.step(planes[lo:hi], pol[lo:hi], val[lo:hi], lr)
             pl_sum += pl
             vl_sum += vl
         t2 = time.perf_counter()
         st = {"iteration": iteration, "replay": len(replay), "new_unique": new_unique, "lr": lr,
               "policy_loss": pl_sum / max(train_steps, 1), "value_loss": vl_sum / max(train_steps, 1),
               "selfplay_s": t1 - t0, "train_s": t2 - t1, "selfplay_games": games_done, "selfplay_sims": sims_done,
-              "games_finished": finished, "episode_steps": steps_done, "moves": moves_done}
+              "games_finished": finished, "episode_steps": steps_done, "moves": moves_done,
+              "shared_replay": shared_replay and world > 1, "shard_batch": shard_batch,
+              "episode_steps_global": steps_global if shared_replay and world > 1 else steps_done}
         history.append(st)
         if log:
             log(st)

@@ -110,9 +110,11 @@ int az_pos_from_fen(const char* fen, az_pos* out) {
     if (*c) sscanf(c, " %d %d", &hm, &fm);
     p.halfmoves = (uint16_t)hm;
     p.fullmoves = (uint16_t)(fm < 1 ? 1 : fm);
+    // shakmaty validates the ep square as written (EnPassant::from_setup) and keeps the
+    // pseudo-legal one: a structurally invalid square is refused, a valid one no pawn can take is
+    // dropped.  Validated before finalize, whose move generator assumes one king per side
     p.ep = azc::pseudo_ep(p, ep);
-    // validated before finalize, whose move generator assumes one king per side
-    if (const char* why = azc::setup_error(p)) return fail(std::string("FEN rejected (") + why + "): " + fen);
+    if (const char* why = azc::setup_error(p, ep)) return fail(std::string("FEN rejected (") + why + "): " + fen);
     bool chk;
     azc::finalize(p, &chk);
     P(out) = p;

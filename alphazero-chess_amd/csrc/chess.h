@@ -57,6 +57,7 @@ constexpr uint64_t DARK = 0xAA55AA55AA55AA55ULL;
 constexpr uint64_t ALL = ~0ULL;
 
 AZ_HD int ctz64(uint64_t b) { return __builtin_ctzll(b); }
+AZ_HD int clz64(uint64_t b) { return __builtin_clzll(b); }
 AZ_HD int popc64(uint64_t b) { return __builtin_popcountll(b); }
 // bitboard accessors with a run-time colour / role: selects over static indices, so a Pos in
 // registers is never indexed dynamically (which would move it to scratch memory on the GPU)
@@ -424,13 +425,27 @@ AZ_HD int finalize(Pos& p, bool* in_check) {
     return n;
 }
 
+// a, b and c on one rank, file, diagonal or anti-diagonal (shakmaty attacks::aligned: c on the
+// line through a and b)
+AZ_HD bool aligned3(int a, int b, int c) {
+    auto r = [](int x) { return x >> 3; };
+    auto f = [](int x) { return x & 7; };
+    return (r(a) == r(b) && r(b) == r(c)) || (f(a) == f(b) && f(b) == f(c)) ||
+           (r(a) - f(a) == r(b) - f(b) && r(b) - f(b) == r(c) - f(c)) ||
+           (r(a) + f(a) == r(b) + f(b) && r(b) + f(b) == r(c) + f(c));
+}
+
 // Why a caller's position is not one shakmaty's Chess::from_setup accepts (its PositionErrorKinds:
 // bitboard consistency, one king per side, too much material, pawns on a back rank, invalid
 // castling rights / ep square, the side not to move in check, impossible check), or nullptr.
 // The reference only ever reaches positions by legal play from Chess::default() (training.rs:344),
 // so these are exactly the positions it can hold; the engine sizes a node's edges for 218 legal
 // moves (az_internal.h MAX_EDGES, search.hip EMAX), which every accepted position respects.
-inline const char* setup_error(const Pos& p) {
+// raw_ep: a FEN's ep square as written (shakmaty validates that one, EnPassant::from_setup; the
+// pseudo-legal square p.ep derives from it is what the position keeps); -1: p.ep itself, which must
+// then also be pseudo-legal (the az_pos invariant for positions passed in as records).
+// Restated from shakmaty 0.29's published validate(); parity unpinned (no fixture holds it).
+inline const char* setup_error(const Pos& p, int raw_ep = -1) {
     const uint64_t w = p.bb[WHITE_BB], b = p.bb[BLACK_BB];
     if (w & b) return "white and black bitboards overlap";
     uint64_t roles = 0;
@@ -457,24 +472,36 @@ inline const char* setup_error(const Pos& p) {
     if (((p.castling & 1) && !has(ROOK, w, 7)) || ((p.castling & 2) && !has(ROOK, w, 0))) return "invalid castling rights";
     if ((p.castling & 12) && !has(KING, b, 60)) return "invalid castling rights";
     if (((p.castling & 4) && !has(ROOK, b, 63)) || ((p.castling & 8) && !has(ROOK, b, 56))) return "invalid castling rights";
-    const uint64_t occ = w | b, empty = ~occ;
-    if (p.ep < 64) {
-        const int ep = p.ep, fwd = p.turn ? 8 : -8;   // the pushed pawn stands one rank beyond ep
+    const uint64_t occ = w | b;
+    const int ep = raw_ep < 0 ? p.ep : raw_ep, fwd = p.turn ? 8 : -8;   // the pushed pawn stands one rank beyond ep
+    if (ep < 64) {
         const uint64_t them = p.turn ? w : b;
         if ((ep >> 3) != (p.turn ? 2 : 5) || (occ & (1ULL << ep)) || (occ & (1ULL << (ep - fwd))) ||
-            !(p.bb[PAWN] & them & (1ULL << (ep + fwd))) || pseudo_ep(p, ep) != ep)
+            !(p.bb[PAWN] & them & (1ULL << (ep + fwd))))
             return "invalid en-passant square";
-    } else if (p.ep != 64) {
+        if (raw_ep < 0 && pseudo_ep(p, ep) != ep) return "en-passant square no pawn can take";
+    } else if (ep != 64) {
         return "invalid en-passant square";
     }
-    auto attackers_of = [&](int color) {   // pieces of !color attacking color's king
-        const uint64_t kbb = p.bb[KING] & (color ? b : w), th = color ? w : b;
+    if (raw_ep >= 0 && p.ep != pseudo_ep(p, raw_ep)) return "en-passant square not the pseudo-legal one";
+    auto attackers_of = [&](int color, uint64_t o) {   // pieces of !color attacking color's king (occupancy o)
+        const uint64_t kbb = p.bb[KING] & (color ? b : w), th = color ? w : b, e = ~o;
         return (pawn_att(color, kbb) & p.bb[PAWN] & th) | (knight_att(kbb) & p.bb[KNIGHT] & th) |
-               (king_att(kbb) & p.bb[KING] & th) | (bishop_att(kbb, empty) & (p.bb[BISHOP] | p.bb[QUEEN]) & th) |
-               (rook_att(kbb, empty) & (p.bb[ROOK] | p.bb[QUEEN]) & th);
+               (king_att(kbb) & p.bb[KING] & th) | (bishop_att(kbb, e) & (p.bb[BISHOP] | p.bb[QUEEN]) & th) |
+               (rook_att(kbb, e) & (p.bb[ROOK] | p.bb[QUEEN]) & th);
     };
-    if (attackers_of(p.turn ^ 1)) return "the side not to move is in check";
-    if (popc64(attackers_of(p.turn)) > 2) return "impossible check";
+    if (attackers_of(p.turn ^ 1, occ)) return "the side not to move is in check";
+    const uint64_t checkers = attackers_of(p.turn, occ);
+    const int ksq = ctz64(p.bb[KING] & (p.turn ? b : w));
+    // two checkers on one line through the king (or more than two) cannot come from one move
+    if (popc64(checkers) > 2 || (popc64(checkers) == 2 && aligned3(ctz64(checkers), ksq, 63 - clz64(checkers))))
+        return "impossible check";
+    if (ep < 64 && checkers) {   // the double push must have given the check: the pushed pawn is the one
+        const int to = ep + fwd, from = ep - fwd;   // checker, or it uncovered one slider's
+        const uint64_t before = (occ & ~(1ULL << to)) | (1ULL << from);
+        if (popc64(checkers) > 1 || ((checkers & ~(1ULL << to)) && attackers_of(p.turn, before)))
+            return "impossible check (en passant)";
+    }
     Pos q = p;
     bool chk;
     if (finalize(q, &chk) > 218) return "more than 218 legal moves";

@@ -614,24 +614,25 @@ __global__ void bn_local_kernel(const float* __restrict__ part, int nb, int C, i
 __global__ void set_value_kernel(float* __restrict__ p, float v) { *p = v; }
 // the ranks' slots -> batch mean / std and the running statistics (momentum 0.1, as
 // finalize_var_kernel); nglob (BN 0 only): the global row count for the loss and the BN backward
-__global__ void bn_global_kernel(const float* __restrict__ xb, int world, int C, int sstride, float* __restrict__ mean,
-                                 float* __restrict__ stdv, float* __restrict__ rmean, float* __restrict__ rvar,
-                                 float* __restrict__ nglob) {
+// coff: the BatchNorm's first channel in the slots (the two head BatchNorms share one exchange)
+__global__ void bn_global_kernel(const float* __restrict__ xb, int world, int C, int sstride, int coff,
+                                 float* __restrict__ mean, float* __restrict__ stdv, float* __restrict__ rmean,
+                                 float* __restrict__ rvar, float* __restrict__ nglob) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= C) return;
     const size_t rs = 2 * (size_t)sstride + 1;
     float n = 0.0f, s = 0.0f;
     for (int r = 0; r < world; r++) {
         n += xb[r * rs + 2 * sstride];
-        s += xb[r * rs + c];
+        s += xb[r * rs + coff + c];
     }
     const float mu = s / n;
     float m2 = 0.0f;
     for (int r = 0; r < world; r++) {
         const float nr = xb[r * rs + 2 * sstride];
         if (nr == 0.0f) continue;
-        const float d = xb[r * rs + c] / nr - mu;
-        m2 += xb[r * rs + sstride + c] + nr * (d * d);
+        const float d = xb[r * rs + coff + c] / nr - mu;
+        m2 += xb[r * rs + sstride + coff + c] + nr * (d * d);
     }
     const float var = m2 / n;
     mean[c] = mu;
@@ -1320,6 +1321,7 @@ struct Trainer {
     int slot = 0;                            // per-BN statistics stride (>= every BN's channels)
     float *tpol = nullptr, *tval = nullptr, *planes = nullptr, *loss = nullptr, *vpart = nullptr;
     float* hloss = nullptr;                  // pinned [Bmax][2]
+    float* hlossx = nullptr;                 // pinned [4]: the losses summed in the gradient all-reduce
     // data parallel: RCCL communicator, or a host-side reducer (az_trainer_set_host_reducer)
     ncclComm_t comm = nullptr;
     az_allreduce_fn host_reduce = nullptr;
@@ -1333,6 +1335,15 @@ struct Trainer {
     bool sharded = false;
     float *xfwd = nullptr, *xback = nullptr, *nglob = nullptr, *lossx = nullptr;
     int xfwd_world = 0;
+    // az_trainer_step in sharded mode: the losses ride in the gradient all-reduce (g[np .. np + 3])
+    bool loss_in_grad = false;
+    float loss_out[2] = {0.0f, 0.0f};
+    // every exchange (collective or host reduction) of the steps since the last read: count, and
+    // HIP events around each one on the trainer stream (a pool of pairs, summed after each step)
+    long long n_exchanges = 0, steps_exchanged = 0;
+    double exchange_ms = 0.0;
+    std::vector<hipEvent_t> xev;
+    int xev_used = 0;
     bool fuse_bn = true;                     // BN apply / backward staged in the next Winograd conv (env AZ_TRAIN_FUSE_BN=0: off)
     // the conv bias gradients of the tower's BatchNorms: bn_back4 partials per BN, summed in one
     // launch at the end of the backward (bias_dst[j] = gradient offset of BN j's conv bias)
@@ -1354,9 +1365,11 @@ struct Trainer {
     }
     ~Trainer() {
         for (hipEvent_t e : ev) if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t e : xev) if (e) (void)hipEventDestroy(e);
         if (comm) ncclCommDestroy(comm);
         for (void* q : allocs) (void)hipFree(q);
         if (hloss) (void)hipHostFree(hloss);
+        if (hlossx) (void)hipHostFree(hlossx);
         if (st) (void)hipStreamDestroy(st);
     }
 };
@@ -1472,14 +1485,35 @@ int nblk_rows(int R) { return (R + tr::CS_ROWS - 1) / tr::CS_ROWS; }
 int host_allreduce(Trainer* T, float* d, size_t n, const char* what);
 // sum of n floats at d over the ranks, on the trainer stream: RCCL, the host reducer, or nothing
 // (one rank)
+constexpr int XEV_PAIRS = 256;
 int exchange(Trainer* T, float* d, size_t n, const char* what) {
+    if (!T->comm && !T->host_reduce) return 0;
+    T->n_exchanges++;
+    hipEvent_t* ev = nullptr;   // events around the exchange (none once the pool is used up)
+    if (T->xev_used < XEV_PAIRS) {
+        if (T->xev.empty()) {
+            T->xev.assign(2 * XEV_PAIRS, nullptr);
+            for (hipEvent_t& e : T->xev) AZ_HIP(hipEventCreate(&e));
+        }
+        ev = &T->xev[2 * T->xev_used++];
+        AZ_HIP(hipEventRecord(ev[0], T->st));
+    }
     if (T->comm) {
         if (ncclAllReduce(d, d, n, ncclFloat, ncclSum, T->comm, T->st) != ncclSuccess)
             return fail(std::string("ncclAllReduce (") + what + ") failed");
-        return 0;
+    } else if (host_allreduce(T, d, n, what)) {
+        return -1;
     }
-    if (T->host_reduce) return host_allreduce(T, d, n, what);
+    if (ev) AZ_HIP(hipEventRecord(ev[1], T->st));
     return 0;
+}
+// after a step's final synchronisation: the exchanges' device time into exchange_ms
+void exchange_times(Trainer* T) {
+    for (int i = 0; i < T->xev_used; i++) {
+        float ms = 0.0f;
+        if (hipEventElapsedTime(&ms, T->xev[2 * i], T->xev[2 * i + 1]) == hipSuccess) T->exchange_ms += ms;
+    }
+    T->xev_used = 0;
 }
 
 // sharded batch: the exchange buffers for the current world (allocated on first use)
@@ -1490,6 +1524,9 @@ int sharded_buffers(Trainer* T) {
     const size_t nf = ((size_t)T->world * (2 * T->slot + 1) + 63) & ~(size_t)63, nb = ((size_t)2 * T->slot + 63) & ~(size_t)63;
     float* q = T->alloc(nf + nb + 128);
     if (!q) return fail("sharded batch: out of device memory");
+    hipPointerAttribute_t pa;
+    if (hipPointerGetAttributes(&pa, q) != hipSuccess || pa.device != T->device)
+        return fail("sharded batch: exchange buffers not on the trainer's device");
     T->xfwd = q;
     T->xback = q + nf;
     T->nglob = T->xback + nb;
@@ -1510,6 +1547,18 @@ bool bn_vec(int C, int ld, std::initializer_list<const float*> ptrs) {
 unsigned bn_grid(int C, int R) {
     const int rs = 256 / (C / 4);
     return (unsigned)std::max(1, std::min((R + rs - 1) / rs, 256 * 4));
+}
+
+// BN bi's normalisation + ReLU (+ residual) with the statistics in its slot: Y -> out
+int bn_apply(Trainer* T, int bi, const float* Y, int ld, int C, int R, size_t bn_off, const float* res, float* out) {
+    const float* P = T->p + bn_off;   // {gamma, beta, running_mean, running_var}
+    const float* mean = T->bmean + (size_t)bi * T->slot;
+    const float* sd = T->bstd + (size_t)bi * T->slot;
+    if (bn_vec(C, ld, {Y, res, out, P, mean, sd}))
+        tr::bn_apply4_kernel<<<bn_grid(C, R), 256, 0, T->st>>>(Y, ld, C, R, mean, sd, P, P + C, res, out);
+    else
+        tr::bn_apply_kernel<<<grid_for((size_t)R * C), 256, 0, T->st>>>(Y, ld, C, R, mean, sd, P, P + C, res, out);
+    return hipGetLastError() == hipSuccess ? 0 : fail("bn forward failed");
 }
 
 // BatchNorm (training) + ReLU (+ residual): Y -> out; saves mean/std in slot `bi`
@@ -1540,7 +1589,7 @@ int bn_forward(Trainer* T, int bi, const float* Y, int ld, int C, int R, size_t 
             tr::set_value_kernel<<<1, 1, 0, T->st>>>(my + 2 * ss, (float)R);
         }
         TRY(exchange(T, T->xfwd, (size_t)T->world * rs, "BatchNorm statistics"));
-        tr::bn_global_kernel<<<(C + 255) / 256, 256, 0, T->st>>>(T->xfwd, T->world, C, ss, mean, sd, P + 2 * C,
+        tr::bn_global_kernel<<<(C + 255) / 256, 256, 0, T->st>>>(T->xfwd, T->world, C, ss, 0, mean, sd, P + 2 * C,
                                                                  P + 3 * C, bi == 0 ? T->nglob : nullptr);
     } else if (bpart) {
         if (R % 64 || ld != C) return fail("bn: board statistics need whole boards");
@@ -1555,11 +1604,34 @@ int bn_forward(Trainer* T, int bi, const float* Y, int ld, int C, int R, size_t 
                              {tr::FIN_VAR, sd, P + 2 * C, P + 3 * C, mean});
     }
     if (!out) return hipGetLastError() == hipSuccess ? 0 : fail("bn statistics failed");
-    if (bn_vec(C, ld, {Y, res, out, P, mean, sd}))
-        tr::bn_apply4_kernel<<<bn_grid(C, R), 256, 0, T->st>>>(Y, ld, C, R, mean, sd, P, P + C, res, out);
-    else
-        tr::bn_apply_kernel<<<grid_for((size_t)R * C), 256, 0, T->st>>>(Y, ld, C, R, mean, sd, P, P + C, res, out);
-    return hipGetLastError() == hipSuccess ? 0 : fail("bn forward failed");
+    return bn_apply(T, bi, Y, ld, C, R, bn_off, res, out);
+}
+
+// sharded: the two head BatchNorms (policy: 32 channels at y40[:, 0:32], value: 8 at y40[:, 32:40],
+// agent.rs:125,134) are independent, so they share ONE exchange -- their rank-local slots side by
+// side, from one 40-channel column sum (a channel's sums do not depend on the width summed), one
+// collective, then each combine (bn_global_kernel at its channel offset) and apply
+int bn_forward_heads_sharded(Trainer* T, int bi, int R, size_t poff, size_t voff) {
+    const int ss = T->slot, rs = 2 * ss + 1, C = 40;
+    float* my = T->xfwd + (size_t)T->rank * rs;
+    float* lmean = T->bmean + (size_t)bi * T->slot;   // scratch: this rank's 40 means (the combine overwrites it)
+    AZ_HIP(hipMemsetAsync(T->xfwd, 0, (size_t)T->world * rs * sizeof(float), T->st));
+    const int nb = nblk_rows(R);
+    dim3 g(nb, 1);
+    tr::launch_colsum<0>(g, T->st, T->y40, 64, C, R, nullptr, nullptr, nullptr, nullptr, T->cpart,
+                         {tr::FIN_SUM, my, nullptr, nullptr, nullptr});
+    tr::finalize_mean_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(T->cpart, nb, C, R, lmean);
+    tr::launch_colsum<1>(g, T->st, T->y40, 64, C, R, lmean, nullptr, nullptr, nullptr, T->cpart,
+                         {tr::FIN_SUM, my + ss, nullptr, nullptr, nullptr});
+    tr::set_value_kernel<<<1, 1, 0, T->st>>>(my + 2 * ss, (float)R);
+    TRY(exchange(T, T->xfwd, (size_t)T->world * rs, "head BatchNorm statistics"));
+    float *Pp = T->p + poff, *Pv = T->p + voff;
+    tr::bn_global_kernel<<<1, 256, 0, T->st>>>(T->xfwd, T->world, 32, ss, 0, T->bmean + (size_t)bi * ss,
+                                               T->bstd + (size_t)bi * ss, Pp + 2 * 32, Pp + 3 * 32, nullptr);
+    tr::bn_global_kernel<<<1, 256, 0, T->st>>>(T->xfwd, T->world, 8, ss, 32, T->bmean + (size_t)(bi + 1) * ss,
+                                               T->bstd + (size_t)(bi + 1) * ss, Pv + 2 * 8, Pv + 3 * 8, nullptr);
+    TRY(bn_apply(T, bi, T->y40, 64, 32, R, poff, nullptr, T->a40));
+    return bn_apply(T, bi + 1, T->y40 + 32, 64, 8, R, voff, nullptr, T->a40 + 32);
 }
 
 // BatchNorm bi applied in the next Winograd conv's staging (statistics from bn_forward(out = null))
@@ -1576,7 +1648,7 @@ int bias_grad(Trainer* T, const float* dy, int ld, int C, int R, float* dst);
 // per-board partials, or column sums), then -- sharded -- their global sums through xback;
 // *ug / *ub: the sums the backward itself uses
 int bn_back_sums(Trainer* T, int bi, const float* dout, const float* O, const float* Y, int ld, int C, int R,
-                 size_t bn_off, const float* bpart, const float** ug_out, const float** ub_out) {
+                 size_t bn_off, const float* bpart, const float** ug_out, const float** ub_out, bool xchg = true) {
     const float* mean = T->bmean + (size_t)bi * T->slot;
     const float* sd = T->bstd + (size_t)bi * T->slot;
     float* dgam = T->g + bn_off;
@@ -1593,7 +1665,7 @@ int bn_back_sums(Trainer* T, int bi, const float* dout, const float* O, const fl
     // the gradient keeps this rank's dgamma / dbeta (summed over ranks with the rest of it);
     // sharded, the BN backward itself needs the global sums: exchanged through xback
     const float *ug = dgam, *ub = dbet;
-    if (T->sharded) {
+    if (T->sharded && xchg) {
         AZ_HIP(hipMemcpyAsync(T->xback, dbet, C * sizeof(float), hipMemcpyDeviceToDevice, T->st));
         AZ_HIP(hipMemcpyAsync(T->xback + C, dgam, C * sizeof(float), hipMemcpyDeviceToDevice, T->st));
         TRY(exchange(T, T->xback, 2 * (size_t)C, "BatchNorm backward sums"));
@@ -1619,15 +1691,40 @@ int bn_back_fused(Trainer* T, int bi, const float* dout, const float* O, const f
     return 0;
 }
 
+int bn_back_apply(Trainer* T, int bi, const float* dout, const float* O, const float* Y, int ld, int C, int R,
+                  size_t bn_off, float* dy, float* dres, float* bias, const float* ug, const float* ub);
 int bn_backward(Trainer* T, int bi, const float* dout, const float* O, const float* Y, int ld, int C, int R,
                 size_t bn_off, float* dy, float* dres, const float* bpart = nullptr, float* bias = nullptr) {
+    const float *ug, *ub;
+    TRY(bn_back_sums(T, bi, dout, O, Y, ld, C, R, bn_off, bpart, &ug, &ub));
+    return bn_back_apply(T, bi, dout, O, Y, ld, C, R, bn_off, dy, dres, bias, ug, ub);
+}
+
+// sharded: the two head BatchNorms' backward sums share ONE exchange (xback = [dbeta_p 32 |
+// dgamma_p 32 | dbeta_v 8 | dgamma_v 8], every piece 16-byte aligned as in bn_back_sums)
+int bn_backward_heads_sharded(Trainer* T, int bi, int R, size_t poff, size_t voff) {
+    const float *ug, *ub;
+    TRY(bn_back_sums(T, bi, T->da40, T->a40, T->y40, 64, 32, R, poff, nullptr, &ug, &ub, false));
+    TRY(bn_back_sums(T, bi + 1, T->da40 + 32, T->a40 + 32, T->y40 + 32, 64, 8, R, voff, nullptr, &ug, &ub, false));
+    const size_t off[4] = {poff + 32, poff, voff + 8, voff};      // dbeta_p, dgamma_p, dbeta_v, dgamma_v
+    const int pos[4] = {0, 32, 64, 72}, cnt[4] = {32, 32, 8, 8};
+    for (int k = 0; k < 4; k++)
+        AZ_HIP(hipMemcpyAsync(T->xback + pos[k], T->g + off[k], cnt[k] * sizeof(float), hipMemcpyDeviceToDevice, T->st));
+    TRY(exchange(T, T->xback, 80, "head BatchNorm backward sums"));
+    TRY(bn_back_apply(T, bi, T->da40, T->a40, T->y40, 64, 32, R, poff, T->dy40, nullptr, nullptr, T->xback + 32,
+                      T->xback));
+    return bn_back_apply(T, bi + 1, T->da40 + 32, T->a40 + 32, T->y40 + 32, 64, 8, R, voff, T->dy40 + 32, nullptr,
+                         nullptr, T->xback + 72, T->xback + 64);
+}
+
+// the element-wise BN backward with the sums ug (dgamma) / ub (dbeta): dy (+ dres), bias partials
+int bn_back_apply(Trainer* T, int bi, const float* dout, const float* O, const float* Y, int ld, int C, int R,
+                  size_t bn_off, float* dy, float* dres, float* bias, const float* ug, const float* ub) {
     const float* mean = T->bmean + (size_t)bi * T->slot;
     const float* sd = T->bstd + (size_t)bi * T->slot;
     float* dgam = T->g + bn_off;
     float* dbet = T->g + bn_off + C;
     const float* nglob = T->sharded ? T->nglob : nullptr;
-    const float *ug, *ub;
-    TRY(bn_back_sums(T, bi, dout, O, Y, ld, C, R, bn_off, bpart, &ug, &ub));
     if (bn_vec(C, ld, {dout, O, Y, dy, dres, T->p + bn_off, dgam, dbet, ug, ub, mean, sd})) {
         const unsigned g = bn_grid(C, R);
         if (bias && (size_t)g * 2 * C > T->bsum_cap) return fail("bn: bias partial buffer too small");
@@ -1654,12 +1751,17 @@ int bias_grad(Trainer* T, const float* dy, int ld, int C, int R, float* dst) {
     return hipGetLastError() == hipSuccess ? 0 : fail("bias grad failed");
 }
 
-int trainer_grads(Trainer* T, const float* planes, const float* tpol, const float* tval, int B, float* losses) {
+// defer_loss (az_trainer_step, sharded): the losses' exchange rides in the gradient all-reduce of
+// the trainer_apply that follows (one dependent collective fewer); they are written there
+int trainer_grads(Trainer* T, const float* planes, const float* tpol, const float* tval, int B, float* losses,
+                  bool defer_loss = false) {
     if (B < 1 || B > T->Bmax) return fail("train: batch size out of range");
     T->last_batch = B;
+    // the current device is per host thread (ranks as threads start on device 0): set it before
+    // anything below allocates or launches
+    AZ_HIP(hipSetDevice(T->device));
     if (T->sharded && sharded_buffers(T)) return -1;
     std::fill(T->bias_pending.begin(), T->bias_pending.end(), 0);
-    AZ_HIP(hipSetDevice(T->device));
     AZ_HIP(hipEventRecord(T->ev[0], T->st));
     const int F = T->F, R = B * 64;
     hipStream_t st = T->st;
@@ -1731,8 +1833,12 @@ int trainer_grads(Trainer* T, const float* planes, const float* tpol, const floa
     const int nbn = 1 + 2 * T->blocks;
     TRY(launch_conv(T, 1, body, F, F, T->w40f, 64, T->b40, nullptr, T->y40, 64, R));
     AZ_HIP(hipMemsetAsync(T->a40, 0, (size_t)R * 64 * sizeof(float), st));
-    TRY(bn_forward(T, nbn, T->y40, 64, 32, R, L.pbn, nullptr, T->a40));
-    TRY(bn_forward(T, nbn + 1, T->y40 + 32, 64, 8, R, L.vbn, nullptr, T->a40 + 32));
+    if (T->sharded) {
+        TRY(bn_forward_heads_sharded(T, nbn, R, L.pbn, L.vbn));
+    } else {
+        TRY(bn_forward(T, nbn, T->y40, 64, 32, R, L.pbn, nullptr, T->a40));
+        TRY(bn_forward(T, nbn + 1, T->y40 + 32, 64, 8, R, L.vbn, nullptr, T->a40 + 32));
+    }
     TRY(launch_conv(T, 1, T->a40, 64, 32, T->wp2f, 64, T->p + L.p2b, nullptr, T->logits, 64, R));
     tr::vflat_kernel<<<grid_for((size_t)B * 512), 256, 0, st>>>(T->a40, T->vflat, B, 0);
     TRY(launch_conv(T, 1, T->vflat, 512, 512, T->p + L.l1w, 64, T->p + L.l1b, nullptr, T->h1, 64, B));
@@ -1761,8 +1867,12 @@ int trainer_grads(Trainer* T, const float* planes, const float* tpol, const floa
     tr::vflat_kernel<<<grid_for((size_t)B * 512), 256, 0, st>>>(T->da40, T->dvflat, B, 1);
     // head BatchNorms -> dy40 (cols >= 40 stay zero)
     AZ_HIP(hipMemsetAsync(T->dy40, 0, (size_t)R * 64 * sizeof(float), st));
-    TRY(bn_backward(T, nbn, T->da40, T->a40, T->y40, 64, 32, R, L.pbn, T->dy40, nullptr));
-    TRY(bn_backward(T, nbn + 1, T->da40 + 32, T->a40 + 32, T->y40 + 32, 64, 8, R, L.vbn, T->dy40 + 32, nullptr));
+    if (T->sharded) {
+        TRY(bn_backward_heads_sharded(T, nbn, R, L.pbn, L.vbn));
+    } else {
+        TRY(bn_backward(T, nbn, T->da40, T->a40, T->y40, 64, 32, R, L.pbn, T->dy40, nullptr));
+        TRY(bn_backward(T, nbn + 1, T->da40 + 32, T->a40 + 32, T->y40 + 32, 64, 8, R, L.vbn, T->dy40 + 32, nullptr));
+    }
     // heads 1x1: dW[F][64] -> policy_conv_1 [32][F], value_conv [8][F]
     TRY(launch_wgrad(T, 1, body, F, F, T->dy40, 64, 64, R, T->dwtmp, (size_t)F * 64));
     tr::transpose_kernel<<<grid_for((size_t)40 * F), 256, 0, st>>>(T->dwtmp, F, 64, T->dwtmp + (size_t)F * 64, F, 40);
@@ -1854,8 +1964,15 @@ int trainer_grads(Trainer* T, const float* planes, const float* tpol, const floa
     double pl = 0.0, vl = 0.0;
     for (int i = 0; i < B; i++) { pl += T->hloss[2 * i]; vl += T->hloss[2 * i + 1]; }
     double nb = B;
+    T->loss_in_grad = false;
     if (T->sharded && (T->comm || T->host_reduce)) {   // means over the global batch
         float h[4] = {(float)pl, (float)vl, (float)B, 0.0f};
+        if (defer_loss) {    // g[np .. np + 3], summed with the gradient (trainer_apply)
+            AZ_HIP(hipMemcpyAsync(T->g + T->np, h, sizeof(h), hipMemcpyHostToDevice, st));
+            AZ_HIP(hipStreamSynchronize(st));
+            T->loss_in_grad = true;
+            return 0;
+        }
         AZ_HIP(hipMemcpyAsync(T->lossx, h, sizeof(h), hipMemcpyHostToDevice, st));
         AZ_HIP(hipStreamSynchronize(st));
         TRY(exchange(T, T->lossx, 4, "losses"));
@@ -1893,12 +2010,12 @@ int trainer_apply(Trainer* T, double lr) {
     AZ_HIP(hipSetDevice(T->device));
     hipStream_t st = T->st;
     AZ_HIP(hipEventRecord(T->ev[1], st));
-    if (T->comm) {   // a 1-rank communicator sums over itself: the identity, through RCCL
-        if (ncclAllReduce(T->g, T->g, T->np, ncclFloat, ncclSum, T->comm, st) != ncclSuccess)
-            return fail("ncclAllReduce (gradients) failed");
-    } else if (T->host_reduce) {
-        if (host_allreduce(T, T->g, T->np, "gradients")) return -1;
-    }
+    // the gradient sum over ranks (a 1-rank communicator sums over itself: the identity, through
+    // RCCL), with the deferred losses in its tail
+    const bool lx = T->loss_in_grad;
+    T->loss_in_grad = false;
+    TRY(exchange(T, T->g, T->np + (lx ? 4 : 0), "gradients"));
+    if (lx) AZ_HIP(hipMemcpyAsync(T->hlossx, T->g + T->np, 4 * sizeof(float), hipMemcpyDeviceToHost, st));
     AZ_HIP(hipEventRecord(T->ev[2], st));
     T->t++;
     const float bc1 = 1.0f - powi_f32(0.9f, T->t), bc2 = 1.0f - powi_f32(0.999f, T->t);
@@ -1912,18 +2029,17 @@ int trainer_apply(Trainer* T, double lr) {
     // same ones, updated from the global batch statistics)
     if ((T->comm || T->host_reduce) && !T->sharded) {
         tr::stats_pack_kernel<<<grid_for(T->nstat), 256, 0, st>>>(T->p, T->stat_idx, T->nstat, T->stat_buf, 0, 1.0f);
-        if (T->comm) {
-            if (ncclAllReduce(T->stat_buf, T->stat_buf, T->nstat, ncclFloat, ncclSum, T->comm, st) != ncclSuccess)
-                return fail("ncclAllReduce (running statistics) failed");
-        } else if (host_allreduce(T, T->stat_buf, (size_t)T->nstat, "running statistics")) {
-            return -1;
-        }
+        TRY(exchange(T, T->stat_buf, (size_t)T->nstat, "running statistics"));
         tr::stats_pack_kernel<<<grid_for(T->nstat), 256, 0, st>>>(T->p, T->stat_idx, T->nstat, T->stat_buf, 1,
                                                                   1.0f / (float)T->world);
     }
     AZ_HIP(hipEventRecord(T->ev[3], st));
     AZ_HIP(hipGetLastError());
     AZ_HIP(hipStreamSynchronize(st));
+    if (lx) {   // the global-batch means (as trainer_grads' separate exchange computes them)
+        T->loss_out[0] = (float)((double)T->hlossx[0] / (double)T->hlossx[2]);
+        T->loss_out[1] = (float)((double)T->hlossx[1] / (double)T->hlossx[2]);
+    }
     float a = 0.0f, b = 0.0f;
     if (hipEventElapsedTime(&a, T->ev[0], T->ev[3]) == hipSuccess &&
         hipEventElapsedTime(&b, T->ev[1], T->ev[2]) == hipSuccess) {
@@ -1931,6 +2047,8 @@ int trainer_apply(Trainer* T, double lr) {
         T->allreduce_ms += b;
         T->steps_timed++;
     }
+    exchange_times(T);
+    if (T->comm || T->host_reduce) T->steps_exchanged++;
     return 0;
 }
 
@@ -1968,7 +2086,7 @@ int az_trainer_create(int blocks, int filters, const float* weights, size_t n, i
     bool ok = hipStreamCreateWithFlags(&T->st, hipStreamNonBlocking) == hipSuccess;
     for (hipEvent_t& e : T->ev) ok = ok && hipEventCreate(&e) == hipSuccess;
     auto A = [&](size_t k) { float* q = T->alloc(k); ok = ok && q; return q; };
-    T->p = A(T->np); T->g = A(T->np); T->m = A(T->np); T->v = A(T->np);
+    T->p = A(T->np); T->g = A(T->np + 4); T->m = A(T->np); T->v = A(T->np);   // g: + the deferred losses
     void* mk = nullptr;
     ok = ok && hipMalloc(&mk, T->np) == hipSuccess;
     if (mk) T->allocs.push_back(mk);
@@ -2016,7 +2134,9 @@ int az_trainer_create(int blocks, int filters, const float* weights, size_t n, i
     T->bsum_cap = (size_t)256 * 4 * 2 * std::max(F, 64);   // bn_grid's workgroup cap x [2][C]
     T->bsum = A(T->bsum_cap);
     if (T->wino) {   // per-BN bias partials of the tower (batched finalize) and the second dy
-        T->bsum_stride = T->bsum_cap;
+        // a slot holds either bn_back4's per-workgroup partials or the fused backward's per-board
+        // ones (B x [2][F]): the larger of the two at max_batch
+        T->bsum_stride = std::max(T->bsum_cap, (size_t)max_batch * 2 * F);
         T->bsum_all = A((size_t)nconv * T->bsum_stride);
         T->bias_pending.assign(nconv, 0);
     }
@@ -2028,6 +2148,7 @@ int az_trainer_create(int blocks, int filters, const float* weights, size_t n, i
     T->planes = A((size_t)max_batch * 19 * 64); T->tpol = A((size_t)max_batch * 4096); T->tval = A(max_batch);
     T->loss = A((size_t)max_batch * 2); T->vpart = A((size_t)max_batch * 65);
     ok = ok && hipHostMalloc((void**)&T->hloss, (size_t)max_batch * 2 * sizeof(float), 0) == hipSuccess;
+    ok = ok && hipHostMalloc((void**)&T->hlossx, 4 * sizeof(float), 0) == hipSuccess;
     if (const char* e = getenv("AZ_TRAIN_FUSE_BN")) T->fuse_bn = atoi(e) != 0;
     if (!ok) { delete T; return fail("az_trainer_create: out of device memory"); }
     // parameters, zero moments, trainable mask (BatchNorm running statistics are not parameters)
@@ -2091,8 +2212,14 @@ int az_trainer_apply(az_trainer* t, double lr) {
 int az_trainer_step(az_trainer* t, const float* planes, const float* target_policy, const float* target_value,
                     int batch, double lr, float* losses) {
     if (!t || !planes || !target_policy || !target_value) return fail("null");
-    if (trainer_grads(t->t, planes, target_policy, target_value, batch, losses) != 0) return -1;
-    return trainer_apply(t->t, lr);
+    if (trainer_grads(t->t, planes, target_policy, target_value, batch, losses, true) != 0) return -1;
+    const bool lx = t->t->loss_in_grad;
+    if (trainer_apply(t->t, lr) != 0) return -1;
+    if (lx && losses) {
+        losses[0] = t->t->loss_out[0];
+        losses[1] = t->t->loss_out[1];
+    }
+    return 0;
 }
 
 int az_trainer_get_params(az_trainer* t, float* out, size_t n) {
@@ -2170,6 +2297,16 @@ int az_trainer_set_comm(az_trainer* t, const void* unique_id, int rank, int worl
 int az_trainer_set_sharded(az_trainer* t, int on) {
     if (!t) return fail("null");
     t->t->sharded = on != 0;
+    return 0;
+}
+
+int az_trainer_exchange_stats(az_trainer* t, int64_t* collectives, int64_t* steps, double* exchange_ms, int reset) {
+    if (!t) return fail("null");
+    Trainer* T = t->t;
+    if (collectives) *collectives = T->n_exchanges;
+    if (steps) *steps = T->steps_exchanged;
+    if (exchange_ms) *exchange_ms = T->exchange_ms;
+    if (reset) { T->n_exchanges = T->steps_exchanged = 0; T->exchange_ms = 0.0; }
     return 0;
 }
 

@@ -132,9 +132,12 @@ def train_child(a):
     val = rng.uniform(-1, 1, B).astype(np.float32)
     sharded = a.train_mode == "sharded"
     if sharded:      # this rank's shard of the one global batch (every rank generated all of it)
-        B //= a.world
-        sl = slice(a.rank * B, (a.rank + 1) * B)
-        planes, pol, val = planes[sl], pol[sl], val[sl]
+        from azchess.training import shard_bounds
+        lo, hi = shard_bounds(B, a.rank, a.world)
+        if hi <= lo:
+            raise SystemExit("--train-batch %d leaves rank %d no rows" % (B, a.rank))
+        B = hi - lo
+        planes, pol, val = planes[lo:hi], pol[lo:hi], val[lo:hi]
     tr = A.Trainer(a.blocks, a.filters, max_batch=B, device=a.device, seed=42)
     if a.world > 1 or sharded:     # sharded at world 1: the 1-rank communicator, so its collectives are timed
         tr.set_comm(bytes.fromhex(a.uid) if a.uid != "-" else A.comm_unique_id(), a.rank, a.world)
@@ -142,12 +145,15 @@ def train_child(a):
     for it in range(2):
         tr.step(planes, pol, val, A.get_cyclical_lr(it))
     tr.timing(reset=True)
+    tr.exchange_stats(reset=True)
     t0 = time.perf_counter()
     for it in range(a.train_steps):
         tr.step(planes, pol, val, A.get_cyclical_lr(it))
     wall = (time.perf_counter() - t0) / a.train_steps
     dev_ms, ar_ms, n = tr.timing()
-    print(json.dumps({"ms_per_step": wall * 1e3, "device_ms_per_step": dev_ms / n, "allreduce_ms_per_step": ar_ms / n}))
+    nx, nxs, xms = tr.exchange_stats()
+    print(json.dumps({"ms_per_step": wall * 1e3, "device_ms_per_step": dev_ms / n, "allreduce_ms_per_step": ar_ms / n,
+                      "rows": B, "collectives_per_step": nx / max(nxs, 1), "exchange_ms_per_step": xms / max(nxs, 1)}))
 
 
 def train_phase(args, A, rank, world, local, mode="per-rank"):
@@ -189,7 +195,7 @@ def train_phase(args, A, rank, world, local, mode="per-rank"):
     if rank != 0:
         return None
     gb = args.train_batch if sharded else args.train_batch * world     # global batch
-    lb = gb // world                                                    # positions per rank
+    lb = -(-gb // world)             # positions of the largest shard (sharded: ranks get floor / ceil)
     flop = 3.0 * net_flop_per_eval(args.blocks, args.filters) * lb
     # executed MFMA work: the residual convs of forward, data grad and weight grad run as Winograd
     # F(2x2,3x3) at F = 256 (train.hip; AZ_TRAIN_WINOGRAD=0 restores direct convs)
@@ -200,8 +206,10 @@ def train_phase(args, A, rank, world, local, mode="per-rank"):
                    (lb, ", gradients all-reduced over RCCL" if world > 1 else ""),
            "mode": mode,
            "mode_note": ("the reference's one batch of %d split over %d rank(s); every BatchNorm's batch statistics "
-                         "and backward sums all-reduced over RCCL (2 collectives per BN per step, plus the losses "
-                         "and the gradient) -- bit-identical to the per-rank step at world 1" % (gb, world))
+                         "and backward sums all-reduced over RCCL (2 collectives per tower BN, one per direction for "
+                         "the two head BNs together, the losses inside the gradient all-reduce) -- bit-identical to "
+                         "the per-rank step at world 1; exchange_ms_per_step times every collective (HIP events on "
+                         "the trainer stream), allreduce_ms_per_step the gradient's alone" % (gb, world))
                         if sharded else
                         ("%d positions per rank, per-rank BatchNorm statistics, gradients averaged over ranks "
                          "(global batch %d)" % (lb, gb)),
@@ -211,6 +219,8 @@ def train_phase(args, A, rank, world, local, mode="per-rank"):
         out.update({"ms_per_step": ms, "samples_per_s": gb / (ms * 1e-3),
                     "device_ms_per_step": res["device_ms_per_step"],
                     "allreduce_ms_per_step": res["allreduce_ms_per_step"],
+                    "rows_rank0": res.get("rows"), "collectives_per_step": res.get("collectives_per_step"),
+                    "exchange_ms_per_step": res.get("exchange_ms_per_step"),
                     "allreduce_bytes": 4 * int(A._lib.lib.az_net_num_params(args.blocks, args.filters)),
                     "achieved_tflops": tf, "peak_tflops": PEAK_F32_TFLOPS, "frac": tf / PEAK_F32_TFLOPS,
                     "executed_flop_per_step": xflop, "residual_convs": "winograd" if wino else "direct",

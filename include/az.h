@@ -295,6 +295,11 @@ int az_trainer_set_host_reducer(az_trainer* t, az_allreduce_fn fn, void* ctx, in
  * BatchNorm statistics and the gradients are averaged (global batch = batch x world).  At one rank
  * both modes compute the same step bit for bit. */
 int az_trainer_set_sharded(az_trainer* t, int on);
+/* the exchanges of the data-parallel steps since the last reset (RCCL all-reduces or host
+ * reductions: sharded BatchNorm statistics and backward sums, losses, gradients, running
+ * statistics): how many, over how many applied steps, and their device time (HIP events around
+ * each one on the trainer stream) */
+int az_trainer_exchange_stats(az_trainer* t, int64_t* collectives, int64_t* steps, double* exchange_ms, int reset);
 
 /* ---- replay buffer: memory.rs ReplayBuffer, host memory ------------ */
 typedef struct az_replay az_replay;

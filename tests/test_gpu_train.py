@@ -417,6 +417,17 @@ def test_sharded_world1_rccl_is_the_plain_step(require_gpu, blocks, filters):
         a.apply(A.get_cyclical_lr(it))
         b.apply(A.get_cyclical_lr(it))
         assert np.array_equal(a.params(), b.params())
+    # az_trainer_step: the losses ride in the gradient all-reduce; the two head BatchNorms share one
+    # exchange per direction -> 2 per tower BN + 2 + 1 collectives per step
+    b.exchange_stats(reset=True)
+    for it in range(2, 4):
+        la = a.step(planes, tpol, tval, A.get_cyclical_lr(it))
+        lb = b.step(planes, tpol, tval, A.get_cyclical_lr(it))
+        assert np.allclose(la, lb, rtol=1e-6, atol=0), (la, lb)
+        assert np.array_equal(a.params(), b.params())
+    n, steps, ms = b.exchange_stats()
+    assert steps == 2 and n == 2 * (2 * (1 + 2 * blocks) + 2 + 1), n
+    assert ms > 0.0
 
 
 @pytest.mark.parametrize("split", [256, 200])
@@ -493,18 +504,109 @@ def test_sharded_world2_host_reducer_matches_single_batch(require_gpu, split):
     assert np.array_equal(got0, want), np.abs(got0 - want).max()
 
 
-def test_train_loop_sharded_two_ranks_host_reducer(require_gpu):
-    """train(shard_batch=True) (training.rs:71-200 with the reference's one batch split over the
-    ranks) for two ranks as threads on one GPU, exchanges through a host reducer: each rank plays its
-    own games into its own replay buffer and samples batch_size / 2 positions per step; the sharded
-    steps apply the same update on both ranks, so the two trainers end with bit-identical
-    parameters (BatchNorm running statistics included), and the losses are finite global means."""
+def _allgather_pair():
+    import threading
+    slots, bar = [None, None], threading.Barrier(2, timeout=120)
+
+    def allgather(rank):
+        def ag(payload):
+            slots[rank] = payload
+            bar.wait()
+            out = list(slots)
+            bar.wait()
+            return out
+        return ag
+    return allgather
+
+
+def test_train_loop_one_global_buffer_two_ranks(require_gpu, tmp_path):
+    """train() at world 2 computes the reference's train() (training.rs:81-159,
+    memory.rs:41-96) -- two ranks as threads on one GPU, gradient / BatchNorm exchanges through a host
+    reducer, EpisodeSteps through an in-process allgather:
+      * each rank plays its own games, and both replicas of the ONE replay buffer end byte-identical
+        (every rank's steps added in (rank, drain) order) and hold both ranks' steps;
+      * every step both ranks draw the same global batch of 64 (shared sample seed) and train the
+        two contiguous halves of it (sharded BatchNorm, the default at world > 1);
+      * the two trainers end bit-identical, and within the sharded tolerance of ONE trainer stepped
+        on the same global batches: losses <= 1e-5 (1 + |l|), BatchNorm running statistics
+        <= 1e-5, the AdamW parameter update <= 1e-2 relative norm (sign flips of near-zero
+        gradients under different ReLU branches, as in the single-step test)."""
+    red, ag = _host_reducer_pair(), _allgather_pair()
+    logs = [[], []]
+    steps, gb, seed = 2, 64, 5
+
+    def run(r):
+        def lb(it, b, planes, pol, val, lo, hi):
+            logs[r].append((planes.copy(), pol.copy(), val.copy(), lo, hi))
+        return A.train(1, blocks=2, filters=256, games=16, sims=8, min_replay=64, train_steps=steps, batch_size=gb,
+                       seed=seed, reducer=(red(r), r, 2), allgather=ag(r), log_batch=lb)
+    out = _run_ranks([lambda r=r: run(r) for r in range(2)])
+    (t0, rep0, h0), (t1, rep1, h1) = out
+    rep0.save(tmp_path / "r0")
+    rep1.save(tmp_path / "r1")
+    assert (tmp_path / "r0").read_bytes() == (tmp_path / "r1").read_bytes()
+    assert h0[0]["shared_replay"] and h0[0]["shard_batch"]
+    assert h0[0]["episode_steps_global"] == h1[0]["episode_steps_global"] == \
+        h0[0]["episode_steps"] + h1[0]["episode_steps"]
+    assert h0[0]["new_unique"] == h1[0]["new_unique"] == len(rep0) >= 64
+    assert h0[0]["policy_loss"] == h1[0]["policy_loss"] and h0[0]["value_loss"] == h1[0]["value_loss"]
+    assert len(logs[0]) == len(logs[1]) == steps
+    for a, b in zip(logs[0], logs[1]):
+        for x, y in zip(a[:3], b[:3]):
+            assert np.array_equal(x, y)                       # the same global batch on both ranks
+        assert a[0].shape[0] == gb and (a[3], a[4], b[3], b[4]) == (0, gb // 2, gb // 2, gb)
+    p0, p1 = t0.params(), t1.params()
+    assert np.array_equal(p0, p1)
+    w0 = A.random_weights(2, 256, seed)
+    one = A.Trainer(2, 256, weights=w0, max_batch=gb)
+    lone = [one.step(pl, po, va, A.get_cyclical_lr(0)) for pl, po, va, _, _ in logs[0]]
+    pone = one.params()
+    for k, name in ((0, "policy_loss"), (1, "value_loss")):
+        want = sum(l[k] for l in lone) / steps
+        assert abs(h0[0][name] - want) <= 1e-5 * (1 + abs(want)), (name, h0[0][name], want)
+    mask = T.trainable_mask(2, 256)
+    st = ~mask
+    assert np.all(np.abs(p0[st] - pone[st]) <= 1e-5 * (1 + np.abs(pone[st])))
+    d_sh, d_one = (p0 - w0)[mask].astype(np.float64), (pone - w0)[mask].astype(np.float64)
+    assert np.linalg.norm(d_sh - d_one) <= 1e-2 * np.linalg.norm(d_one), np.linalg.norm(d_sh - d_one) / np.linalg.norm(d_one)
+
+
+def test_train_loop_per_rank_opt_in_two_ranks(require_gpu):
+    """The labelled opt-ins (shared_replay=False, shard_batch=False): each rank its own buffer and
+    its own batch of batch_size, per-rank BatchNorm, averaged gradients -- the trainers still end
+    bit-identical and the losses are finite."""
     red = _host_reducer_pair()
-    out = _run_ranks([lambda r=r: A.train(1, blocks=2, filters=256, games=16, sims=8, min_replay=64, train_steps=3,
-                                          batch_size=64, seed=5, reducer=(red(r), r, 2), shard_batch=True)
+    out = _run_ranks([lambda r=r: A.train(1, blocks=2, filters=256, games=16, sims=8, min_replay=64, train_steps=2,
+                                          batch_size=32, seed=5, reducer=(red(r), r, 2), shard_batch=False,
+                                          shared_replay=False)
                       for r in range(2)])
     (t0, rep0, h0), (t1, rep1, h1) = out
-    assert h0[0]["policy_loss"] == h1[0]["policy_loss"] and h0[0]["value_loss"] == h1[0]["value_loss"]
+    assert not h0[0]["shared_replay"] and not h0[0]["shard_batch"]
     assert np.isfinite(h0[0]["policy_loss"]) and np.isfinite(h0[0]["value_loss"])
     assert np.array_equal(t0.params(), t1.params())
     assert len(rep0) >= 64 and len(rep1) >= 64
+
+
+def test_winograd_trainer_more_than_1024_positions(require_gpu):
+    """the fused BN backward keeps per-board bias partials (B x [2][F]) in slots sized for
+    max_batch, so a Winograd trainer takes more than 1024 positions per step; its gradients equal
+    the unfused backward's (AZ_TRAIN_FUSE_BN=0) within 1e-5 relative norm."""
+    import os
+    w = A.random_weights(1, 256, seed=61)
+    planes, tpol, tval = batch(1100, seed=62)
+    a = A.Trainer(1, 256, weights=w, max_batch=1100)
+    la = a.compute_gradients(planes, tpol, tval)
+    old = os.environ.get("AZ_TRAIN_FUSE_BN")
+    os.environ["AZ_TRAIN_FUSE_BN"] = "0"
+    try:
+        b = A.Trainer(1, 256, weights=w, max_batch=1100)
+    finally:
+        if old is None:
+            del os.environ["AZ_TRAIN_FUSE_BN"]
+        else:
+            os.environ["AZ_TRAIN_FUSE_BN"] = old
+    lb = b.compute_gradients(planes, tpol, tval)
+    assert np.allclose(la, lb, rtol=1e-6), (la, lb)
+    ga, gb = a.grads().astype(np.float64), b.grads().astype(np.float64)
+    assert np.all(np.isfinite(ga))
+    assert np.linalg.norm(ga - gb) <= 1e-5 * np.linalg.norm(gb), np.linalg.norm(ga - gb) / np.linalg.norm(gb)

@@ -16,7 +16,8 @@ EDGE_FENS = [
     "rnbq1k1r/pp1Pbppp/2p5/8/2B5/8/PPP1NnPP/RNBQK2R w KQ - 1 8",
     "8/8/8/2k5/3Pp3/8/8/4K3 b - d3 0 1",          # ep available
     "8/8/8/8/k2Pp2Q/8/8/3K4 b - d3 0 1",          # ep illegal (horizontal pin)
-    "8/8/8/1k6/3Pp3/8/8/4KQ2 b - d3 0 1",
+    "8/8/8/2k5/3Pp3/8/8/4KQ2 b - d3 0 1",         # in check by the pushed pawn: ep takes it (round 6: the
+                                                  # earlier queen-check version is an impossible check)
     "4k3/8/8/8/8/8/8/R3K2R w KQ - 0 1",
     "r3k2r/8/8/8/8/8/8/R3K2R b KQkq - 0 1",
     "r3k2r/8/8/8/8/5q2/8/R3K2R w KQkq - 0 1",      # castling through check
@@ -87,23 +88,45 @@ BAD_FENS = [
     "4k3/8/8/8/8/8/PPPPPPPP/P3K3 w - - 0 1",             # 9 pawns, one on the back rank
     "4k3/8/8/8/8/8/8/P3K3 w - - 0 1",                    # pawn on the first rank
     "4k3/8/8/8/8/8/4R3/4K3 w - - 0 1",                   # side not to move in check
-    "4k3/8/8/8/8/8/8/4K3 w - e6 0 1",                    # ep square without the pushed pawn... (dropped: no capturer)
+    "4k3/8/8/8/8/8/8/4K3 w - e6 0 1",                    # ep square without the pushed pawn (refused)
     "4k3/8/8/3P4/8/8/8/4K3 w - e6 0 1",                   # ep square a pawn could take, no pushed pawn
     "8/8/8/8/8/8/8/8 w - - 0 1",                         # no kings
     "k7/8/8/8/8/8/8/KK6 w - - 0 1",                      # two white kings
     "4k3/8/8/8/8/5n2/3b4/r3K3 w - - 0 1",                # triple check
+    "4r3/8/8/8/4K3/8/8/k3r3 w - - 0 1",                  # two checkers on one line through the king (rooks e8, e1)
+    "7k/6q1/8/8/3K4/8/8/b7 w - - 0 1",                    # ... on one diagonal (bishop a1, queen g7)
+    "k6R/8/8/8/4P3/8/8/4K3 b - e3 0 1",                  # check the double push e2-e4 could not have given
+    "8/8/8/6k1/3PN3/8/8/2B1K3 b - d3 0 1",                # ep with two checkers (the push uncovered one)
+    "8/8/8/1k6/3Pp3/8/8/4KQ2 b - d3 0 1",                 # ep, and a queen check the push did not uncover
 ]
 
 
-@pytest.mark.parametrize("fen", [f for i, f in enumerate(BAD_FENS) if i != 5])
+@pytest.mark.parametrize("fen", BAD_FENS)
 def test_invalid_setups_refused(fen):
     with pytest.raises(L.AzError):
         A.Position.from_fen(fen)
 
 
 def test_ep_without_capturer_is_dropped_not_refused():
-    # shakmaty keeps only a pseudo-legal ep square; one no pawn can take is simply absent
-    assert A.Position.from_fen(BAD_FENS[5]).fen() == "4k3/8/8/8/8/8/8/4K3 w - - 0 1"
+    """shakmaty validates the ep square as written (pushed pawn present, its squares empty) and keeps
+    only the pseudo-legal one: a valid square no pawn can take is absent from the position.
+    Restated from shakmaty 0.29 (EnPassant::from_setup); parity unpinned -- the reference only
+    parses FENs of positions it produced itself (memory.rs:90)."""
+    assert A.Position.from_fen("4k3/8/8/8/4P3/8/8/4K3 b - e3 0 1").fen() == "4k3/8/8/8/4P3/8/8/4K3 b - - 0 1"
+
+
+@pytest.mark.parametrize("fen,ep", [
+    ("8/8/8/6k1/3P4/8/8/2B1K3 b - d3 0 1", "-"),         # the push d2-d4 uncovered the bishop's check
+    ("8/8/8/8/3Pp3/8/8/k3K3 b - d3 0 1", "d3"),           # no check, a pawn can take: kept
+    ("8/8/8/2k5/3P4/8/8/4K3 b - d3 0 1", "-"),           # the pushed pawn itself gives check
+])
+def test_possible_ep_checks_accepted(fen, ep):
+    assert A.Position.from_fen(fen).fen().split()[3] == ep
+
+
+def test_aligned_checker_rule_is_about_one_line():
+    # a knight and a rook check from different lines: a legal double check
+    assert A.Position.from_fen("4k3/8/8/8/8/5n2/8/4rK2 w - - 0 1") is not None
 
 
 def test_probe_refuses_bad_parent_before_any_device_call():
