@@ -896,6 +896,7 @@ struct BoardStats {
     const float* Ybn;    // STATS 2: the BN's input
     const float* mean;   // STATS 2
     const float* stdv;   // STATS 2
+    const float *gamma, *beta;   // STATS 2 with ORC & 2: O's sign recomputed from Ybn (no residual)
 };
 // BNIN: the conv's input is the BatchNorm + ReLU (+ residual) of the previous conv's output,
 // applied while the board's rows are staged (bn_apply4_kernel's arithmetic, element for element),
@@ -914,7 +915,17 @@ struct BnBack {
     const float *O, *Y, *mean, *stdv, *gamma, *dgamma, *dbeta, *nglob;
     float *dy, *dres, *bsum;
     int R;
+    const float* beta;   // ORC & 1: O's sign recomputed from Y (no residual)
 };
+// ORC (round 6): a BatchNorm with no residual (BN 0 and every block's BN1) has O = relu(v) with
+// v = ((Y - mean) / std) * gamma + beta, the exact float expression the forward evaluated (BnIn staging
+// or bn_apply4_kernel, -ffp-contract=off), so O > 0 <=> v > 0 and the backward need not read O:
+// bit 0 -- the BN backward in the staging (BnBack), bit 1 -- the STATS 2 epilogue (BoardStats).
+// Each drops one of the three 64 KB-per-board streams of its phase (the staging and the epilogue
+// are bound by HBM bandwidth: every CU runs them at the same moment).
+__device__ __forceinline__ bool relu_pos(float y, float mu, float sd, float ga, float be) {
+    return ((y - mu) / sd) * ga + be > 0.0f;
+}
 __device__ __forceinline__ f32x4 sum16(f32x4 v) {   // over the 16 lanes of a row (fixed butterfly)
 #pragma unroll
     for (int m = 1; m < 16; m <<= 1)
@@ -922,7 +933,7 @@ __device__ __forceinline__ f32x4 sum16(f32x4 v) {   // over the 16 lanes of a ro
         for (int r = 0; r < 4; r++) v[r] += __shfl_xor(v[r], m, 64);
     return v;
 }
-template <bool ADD, int STATS, int XIN>
+template <bool ADD, int STATS, int XIN, int ORC = 0>
 __global__ void __launch_bounds__(512)
 conv_wino_train_kernel(const float* __restrict__ X, const uint4* __restrict__ U, unsigned ubytes,
                        const float* __restrict__ bias, const float* __restrict__ addend, float* __restrict__ Y,
@@ -989,15 +1000,24 @@ conv_wino_train_kernel(const float* __restrict__ X, const uint4* __restrict__ U,
             const float4 mu = reinterpret_cast<const float4*>(bb.mean)[cq], sd = reinterpret_cast<const float4*>(bb.stdv)[cq];
             const float4 ga = reinterpret_cast<const float4*>(bb.gamma)[cq], dg = reinterpret_cast<const float4*>(bb.dgamma)[cq];
             const float4 db = reinterpret_cast<const float4*>(bb.dbeta)[cq];
+            float4 be = make_float4(0.f, 0.f, 0.f, 0.f);
+            if constexpr ((ORC & 1) != 0) be = reinterpret_cast<const float4*>(bb.beta)[cq];
             const size_t o0 = row0 * (F / 4);
             float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
             for (int k = 0; k < 8; k++) {
                 const size_t c = o0 + tid + 512 * k;
-                const float4 d = reinterpret_cast<const float4*>(X)[c], ov = reinterpret_cast<const float4*>(bb.O)[c];
+                const float4 d = reinterpret_cast<const float4*>(X)[c];
                 const float4 y = reinterpret_cast<const float4*>(bb.Y)[c];
-                const float4 dz = make_float4(ov.x > 0.0f ? d.x : 0.0f, ov.y > 0.0f ? d.y : 0.0f, ov.z > 0.0f ? d.z : 0.0f,
-                                              ov.w > 0.0f ? d.w : 0.0f);
+                bool px, py, pz, pw;   // O > 0
+                if constexpr ((ORC & 1) != 0) {
+                    px = relu_pos(y.x, mu.x, sd.x, ga.x, be.x); py = relu_pos(y.y, mu.y, sd.y, ga.y, be.y);
+                    pz = relu_pos(y.z, mu.z, sd.z, ga.z, be.z); pw = relu_pos(y.w, mu.w, sd.w, ga.w, be.w);
+                } else {
+                    const float4 ov = reinterpret_cast<const float4*>(bb.O)[c];
+                    px = ov.x > 0.0f; py = ov.y > 0.0f; pz = ov.z > 0.0f; pw = ov.w > 0.0f;
+                }
+                const float4 dz = make_float4(px ? d.x : 0.0f, py ? d.y : 0.0f, pz ? d.z : 0.0f, pw ? d.w : 0.0f);
                 const float4 d4 = make_float4((ga.x / sd.x) * (dz.x - db.x * invR - ((y.x - mu.x) / sd.x) * dg.x * invR),
                                               (ga.y / sd.y) * (dz.y - db.y * invR - ((y.y - mu.y) / sd.y) * dg.y * invR),
                                               (ga.z / sd.z) * (dz.z - db.z * invR - ((y.z - mu.z) / sd.z) * dg.z * invR),
@@ -1035,10 +1055,14 @@ conv_wino_train_kernel(const float* __restrict__ X, const uint4* __restrict__ U,
         for (int n = 0; n < NN; n++) {
             s0[n] = f32x4{0.f, 0.f, 0.f, 0.f};
             s1[n] = s0[n];
-            f32x4 mu = s0[n], sd = s0[n];
+            f32x4 mu = s0[n], sd = s0[n], ga = s0[n], be = s0[n];
             if constexpr (STATS == 2) {
                 mu = *reinterpret_cast<const f32x4*>(bs.mean + co0 + n * 16);
                 sd = *reinterpret_cast<const f32x4*>(bs.stdv + co0 + n * 16);
+                if constexpr ((ORC & 2) != 0) {
+                    ga = *reinterpret_cast<const f32x4*>(bs.gamma + co0 + n * 16);
+                    be = *reinterpret_cast<const f32x4*>(bs.beta + co0 + n * 16);
+                }
             }
 #pragma unroll
             for (int q = 0; q < 4; q++) {
@@ -1050,11 +1074,13 @@ conv_wino_train_kernel(const float* __restrict__ X, const uint4* __restrict__ U,
                     y[n][q] = v;
                     s0[n] += v;
                 } else if constexpr (STATS == 2) {
-                    const f32x4 ov = *reinterpret_cast<const f32x4*>(bs.O + o);
+                    f32x4 ov = s0[n];
+                    if constexpr ((ORC & 2) == 0) ov = *reinterpret_cast<const f32x4*>(bs.O + o);
                     const f32x4 yb = *reinterpret_cast<const f32x4*>(bs.Ybn + o);
 #pragma unroll
                     for (int r = 0; r < 4; r++) {
-                        const float dz = ov[r] > 0.0f ? v[r] : 0.0f;
+                        const bool pos = (ORC & 2) != 0 ? relu_pos(yb[r], mu[r], sd[r], ga[r], be[r]) : ov[r] > 0.0f;
+                        const float dz = pos ? v[r] : 0.0f;
                         s0[n][r] += dz;
                         s1[n][r] += dz * ((yb[r] - mu[r]) / sd[r]);
                     }
@@ -1345,6 +1371,7 @@ struct Trainer {
     std::vector<hipEvent_t> xev;
     int xev_used = 0;
     bool fuse_bn = true;                     // BN apply / backward staged in the next Winograd conv (env AZ_TRAIN_FUSE_BN=0: off)
+    bool orc = true;                         // O's sign recomputed where no residual (env AZ_TRAIN_ORC=0: off)
     // the conv bias gradients of the tower's BatchNorms: bn_back4 partials per BN, summed in one
     // launch at the end of the backward (bias_dst[j] = gradient offset of BN j's conv bias)
     float* bsum_all = nullptr;
@@ -1413,12 +1440,24 @@ int launch_wino(Trainer* T, const float* X, const float* U, const float* bias, c
     }
 #endif
     const unsigned wg = (unsigned)std::min(B, AZ_TRAIN_WG);   // persistent workgroups (one per CU)
+    // ORC: O's sign recomputed (no residual: BN 0 and BN1s) where the host asks for it
+    const int orc = (bb.dy && bb.beta ? 1 : 0) | (stats == 2 && bs.gamma ? 2 : 0);
     if (bn.out)
         tr::conv_wino_train_kernel<false, 1, 1><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb);
+    else if (bb.dy && addend && orc == 1)   // conv1's data grad: BN1's backward, BN 2b's statistics
+        tr::conv_wino_train_kernel<true, 2, 2, 1><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, trb);
+    else if (bb.dy && addend && orc == 3)   // ... of block 0 (BN 0 has no residual either)
+        tr::conv_wino_train_kernel<true, 2, 2, 3><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, trb);
+    else if (bb.dy && !addend && orc == 2)  // conv2's data grad: BN2's backward, BN1's statistics
+        tr::conv_wino_train_kernel<false, 2, 2, 2><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb);
     else if (bb.dy && addend)
         tr::conv_wino_train_kernel<true, 2, 2><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, trb);
     else if (bb.dy)
         tr::conv_wino_train_kernel<false, 2, 2><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb);
+    else if (stats == 2 && bs.gamma && addend)   // unfused backward (AZ_TRAIN_FUSE_BN=0), conv1's data grad
+        tr::conv_wino_train_kernel<true, 2, 0, 2><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, trb);
+    else if (stats == 2 && bs.gamma)             // ... conv2's
+        tr::conv_wino_train_kernel<false, 2, 0, 2><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb);
     else if (addend && stats == 2)
         tr::conv_wino_train_kernel<true, 2, 0><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, trb);
     else if (addend && stats == 0)
@@ -1460,11 +1499,14 @@ int launch_wgrad(Trainer* T, int taps, const float* X, int ldx, int K, const flo
 }
 
 // Winograd weight grad of a residual F x F conv (input X, output gradient DY, B boards) into g
-// F = 256 (wino_wgrad_gemm_kernel): 512 rows per split, 16 x 16 = 256 workgroups at B = 512
-constexpr int WINO_GEMM_ROWS = 512;
-size_t wino_gemm_splits(int B) { return (size_t)((B * 16 + WINO_GEMM_ROWS - 1) / WINO_GEMM_ROWS); }
-// Winograd weight grad (F = 256, the only Winograd training width: T->wino): the transforms fused
-// into the GEMM's staging (wino_wgrad_gemm_kernel), the splits summed in order, dW = G^T dU G
+// F = 256 (wino_wgrad_gemm_kernel): the (board, tile) rows split into at most 16 splits of whole
+// boards, 16 points each: 256 workgroups at B = 512 (512 rows per split), and still 256 at the
+// 64 positions per rank of a world-8 sharded step (64 rows per split; round 6 -- a fixed 512-row
+// split left 32 workgroups there, as slow as the whole 512 batch)
+constexpr int WINO_GEMM_SPLITS = 16;
+int wino_gemm_rows(int B) { return 16 * ((B + WINO_GEMM_SPLITS - 1) / WINO_GEMM_SPLITS); }
+size_t wino_gemm_splits(int B) { return (size_t)((B * 16 + wino_gemm_rows(B) - 1) / wino_gemm_rows(B)); }
+size_t wino_gemm_splits_max(int Bmax) { return (size_t)std::min(Bmax, WINO_GEMM_SPLITS); }   // over B <= Bmax
 int launch_wino_wgrad(Trainer* T, const float* X, const float* DY, int B, float* g) {
     const int F = T->F, K = B * 16;
     if (F != 256) return fail("Winograd wgrad: F = 256 only");
@@ -1474,7 +1516,7 @@ int launch_wino_wgrad(Trainer* T, const float* X, const float* DY, int B, float*
     if ((size_t)B * 64 * F * 4 >= (size_t)0x40000000) return fail("Winograd wgrad: batch too large for 32-bit offsets");
     if ((size_t)F * F % 256) return fail("Winograd wgrad: F * F must be a multiple of 256");
     const unsigned rblocks = (unsigned)((size_t)F * F / 256);
-    tr::wino_wgrad_gemm_kernel<<<dim3(splits, 16), 512, 0, T->st>>>(X, DY, K, WINO_GEMM_ROWS, T->wpart);
+    tr::wino_wgrad_gemm_kernel<<<dim3(splits, 16), 512, 0, T->st>>>(X, DY, K, wino_gemm_rows(B), T->wpart);
     tr::wino_wgrad_reduce_out_kernel<<<rblocks, 1024, 0, T->st>>>(T->wpart, splits, F, g);
     return hipGetLastError() == hipSuccess ? 0 : fail("Winograd wgrad launch failed");
 }
@@ -1685,8 +1727,11 @@ int bn_back_fused(Trainer* T, int bi, const float* dout, const float* O, const f
     const float *ug, *ub;
     TRY(bn_back_sums(T, bi, dout, O, Y, C, C, R, bn_off, bpart, &ug, &ub));
     if ((size_t)B * 2 * C > T->bsum_stride || bi >= (int)T->bias_pending.size()) return fail("bn: fused backward: bad shape");
+    // BN 0 and the BN1s have no residual: the staging recomputes O's sign from Y (tr ORC bit 0)
+    const bool orc = T->orc && (bi == 0 || bi % 2 == 1);
     *bb = tr::BnBack{O, Y, T->bmean + (size_t)bi * T->slot, T->bstd + (size_t)bi * T->slot, T->p + bn_off, ug, ub,
-                     T->sharded ? T->nglob : nullptr, dy, dres, T->bsum_all + (size_t)bi * T->bsum_stride, R};
+                     T->sharded ? T->nglob : nullptr, dy, dres, T->bsum_all + (size_t)bi * T->bsum_stride, R,
+                     orc ? T->p + bn_off + C : nullptr};
     T->bias_pending[bi] = B;     // partials per board
     return 0;
 }
@@ -1892,7 +1937,11 @@ int trainer_grads(Trainer* T, const float* planes, const float* tpol, const floa
         const auto& c1 = L.tower[1 + 2 * b];
         const auto& c2 = L.tower[2 + 2 * b];
         auto bstat = [&](int bi, const float* O, const float* Ybn) {
-            return tr::BoardStats{T->bpart, O, Ybn, T->bmean + (size_t)bi * T->slot, T->bstd + (size_t)bi * T->slot};
+            // BN 0 and the BN1s have no residual: the epilogue recomputes O's sign (tr ORC bit 1)
+            const bool orc = T->orc && (bi == 0 || bi % 2 == 1);
+            const float* ga = orc ? T->p + L.tower[bi].bn : nullptr;
+            return tr::BoardStats{T->bpart, O, Ybn, T->bmean + (size_t)bi * T->slot, T->bstd + (size_t)bi * T->slot, ga,
+                                  orc ? ga + F : nullptr};
         };
         if (fuseb) {
             // BN2's backward (dout = dx) in conv2's data grad: dy (read by conv2's weight grad
@@ -2125,7 +2174,7 @@ int az_trainer_create(int blocks, int filters, const float* weights, size_t n, i
     wp = std::max(wp, s1 * 32 * 64);                                    // policy_conv_2
     wp = std::max(wp, sl * 512 * 64);                                   // value_linear_1
     if (T->wino) {   // Winograd weight grads: [16][Bmax * 16][F] transforms, dU [16][F][F]
-        wp = std::max(wp, wino_gemm_splits(max_batch) * 16 * (size_t)F * F);
+        wp = std::max(wp, wino_gemm_splits_max(max_batch) * 16 * (size_t)F * F);
     }
     T->wpart_cap = wp;
     T->wpart = A(wp);
@@ -2150,6 +2199,7 @@ int az_trainer_create(int blocks, int filters, const float* weights, size_t n, i
     ok = ok && hipHostMalloc((void**)&T->hloss, (size_t)max_batch * 2 * sizeof(float), 0) == hipSuccess;
     ok = ok && hipHostMalloc((void**)&T->hlossx, 4 * sizeof(float), 0) == hipSuccess;
     if (const char* e = getenv("AZ_TRAIN_FUSE_BN")) T->fuse_bn = atoi(e) != 0;
+    if (const char* e = getenv("AZ_TRAIN_ORC")) T->orc = atoi(e) != 0;
     if (!ok) { delete T; return fail("az_trainer_create: out of device memory"); }
     // parameters, zero moments, trainable mask (BatchNorm running statistics are not parameters)
     std::vector<uint8_t> mask(T->np, 1);

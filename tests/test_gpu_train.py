@@ -271,14 +271,14 @@ def test_bn_staging_matches_separate_bn_kernels(require_gpu, monkeypatch, blocks
 
 
 def test_winograd_weight_grad_multi_split(require_gpu):
-    """the production Winograd weight grad (wino_wgrad_gemm_kernel, 512 rows of
-    (board, tile) per split, the splits summed by wino_wgrad_reduce_out_kernel) with more than one
-    split: 80 boards = 1280 rows = 3 splits, the last one partial.  Every gradient tensor against
+    """the production Winograd weight grad (wino_wgrad_gemm_kernel, at most 16 splits of
+    whole boards, summed by wino_wgrad_reduce_out_kernel) with a partial last split: 81 boards =
+    14 splits of 6 boards, the last one of 3.  Every gradient tensor against
     the float64 oracle under the GPU's ReLU masks (1e-4 relative norm), at F = 256 where that kernel
     runs.  The same batch pins the per-board BatchNorm statistics of the Winograd conv epilogues
-    (round 4: forward sums / squared deviations combined over 80 boards, backward dz sums): the
+    (round 4: forward sums / squared deviations combined over 81 boards, backward dz sums): the
     BN gamma / beta grads above and the running statistics below."""
-    blocks, filters, n = 2, 256, 80
+    blocks, filters, n = 2, 256, 81
     w = A.random_weights(blocks, filters, seed=13)
     planes, tpol, tval = batch(n, seed=81)
     tr = A.Trainer(blocks, filters, weights=w, max_batch=n)
