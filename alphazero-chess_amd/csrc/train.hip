@@ -1504,9 +1504,12 @@ int launch_wgrad(Trainer* T, int taps, const float* X, int ldx, int K, const flo
 // 64 positions per rank of a world-8 sharded step (64 rows per split; round 6 -- a fixed 512-row
 // split left 32 workgroups there, as slow as the whole 512 batch)
 constexpr int WINO_GEMM_SPLITS = 16;
-int wino_gemm_rows(int B) { return 16 * ((B + WINO_GEMM_SPLITS - 1) / WINO_GEMM_SPLITS); }
+int g_wgrad_rows = 0;   // A/B only (env AZ_TRAIN_WGRAD_ROWS): a fixed split size in rows (round 5: 512)
+int wino_gemm_rows(int B) { return g_wgrad_rows > 0 ? g_wgrad_rows : 16 * ((B + WINO_GEMM_SPLITS - 1) / WINO_GEMM_SPLITS); }
 size_t wino_gemm_splits(int B) { return (size_t)((B * 16 + wino_gemm_rows(B) - 1) / wino_gemm_rows(B)); }
-size_t wino_gemm_splits_max(int Bmax) { return (size_t)std::min(Bmax, WINO_GEMM_SPLITS); }   // over B <= Bmax
+size_t wino_gemm_splits_max(int Bmax) {   // over B <= Bmax
+    return g_wgrad_rows > 0 ? wino_gemm_splits(Bmax) : (size_t)std::min(Bmax, WINO_GEMM_SPLITS);
+}
 int launch_wino_wgrad(Trainer* T, const float* X, const float* DY, int B, float* g) {
     const int F = T->F, K = B * 16;
     if (F != 256) return fail("Winograd wgrad: F = 256 only");
@@ -2173,6 +2176,7 @@ int az_trainer_create(int blocks, int filters, const float* weights, size_t n, i
     wp = std::max(wp, s1 * (size_t)F * 64);                             // heads 1x1
     wp = std::max(wp, s1 * 32 * 64);                                    // policy_conv_2
     wp = std::max(wp, sl * 512 * 64);                                   // value_linear_1
+    if (const char* e = getenv("AZ_TRAIN_WGRAD_ROWS")) g_wgrad_rows = std::max(0, atoi(e) / 16 * 16);
     if (T->wino) {   // Winograd weight grads: [16][Bmax * 16][F] transforms, dU [16][F][F]
         wp = std::max(wp, wino_gemm_splits_max(max_batch) * 16 * (size_t)F * F);
     }

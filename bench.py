@@ -60,7 +60,7 @@ def pmc_traffic(games, blocks, filters, dtype, winograd=True):
     return s.get("traffic_bytes"), os.path.relpath(path, ROOT)
 
 
-def cpu_baseline(blocks, filters, threads, games, sims):
+def cpu_baseline(blocks, filters, threads, games, sims, port=True):
     """The reference's self-play on the host cores, a bounded sample of the same workload: `games`
     games from the start position, one move of `sims` simulations each, same 20x256 net (seed 42).
     Batched like the reference's batcher (training.rs:340-422): the oracle's trees (dense 4096
@@ -97,6 +97,8 @@ def cpu_baseline(blocks, filters, threads, games, sims):
                      "simulation step (torch-CPU oneDNN, BN folded), %dx%d net, %d threads, %.1f s"
                      % (games, sims, blocks, filters, threads, dt),
            "evals": nevals}
+    if not port:
+        return out
     rnet = O.RefNet(blocks, filters, w)
     pcfg = O.make_cfg(sims=max(sims // 4, 1), noise=True, seed=42, eval_kind=1, net=rnet, threads=threads)
     t0 = time.perf_counter()
@@ -701,7 +703,11 @@ def main():
                   "note": "the whole network's direct-conv FLOPs (SURVEY 8a A6, heads included) / tower time: an "
                           "equivalent rate, not a fraction of a peak (roofline.frac is the executed-MFMA fraction)",
                   "ms_per_sim_step": tm["tower_ms"] / max(tm["sim_steps"], 1),
-                  "share_of_step": (tm["tower_ms"] / max(tm["sim_steps"], 1)) * K / (elapsed / args.steps * 1e3)},
+                  "share_of_step": (tm["tower_ms"] / max(tm["sim_steps"], 1)) * K / (elapsed / args.steps * 1e3),
+                  "share_note": "sampled launches (HIP events around every 32nd launch) x launches per step / wall time "
+                                "per step; the event-bracketed launch starts on an idle pipe, so it can run ~0.5 % "
+                                "longer than the average in-stream launch and this share can exceed 1 by that much "
+                                "(roofline.achieved_wall_bound has no such bias)"},
         "tolerance_vs_f32_oracle": TOLERANCE[args.dtype],
         "bf16_mode": bf16_res,
         "tree_walk": {"kernel": "k_select", "achieved_gbs": sel_gbs, "peak_gbs": PEAK_HBM_GBS,
@@ -744,11 +750,30 @@ def main():
             "note": "projection, not a measurement: measured sims/s / (800 sims x mean plies of %d complete games "
                     "of a separate run); the timed window (%d x %d simulation steps) is too short for games to "
                     "finish" % (gl["games"], args.steps, K)}
+    if roof and not args.rehearse and not tm.get("persistent") and elapsed > 0:
+        # a bound free of the event bias: every launch of the window took at most wall / launches
+        # (the tower is one of two launches per simulation step), so the executed rate is at least
+        rpl = roof["rows_per_launch"]
+        wb = roof["executed_flop_per_row"] * rpl * K * args.steps / elapsed / 1e12
+        roof["achieved_wall_bound"] = wb
+        roof["frac_wall_bound"] = wb / roof["peak"]
+        roof["wall_bound_note"] = ("executed MFMA FLOPs of every tower launch of the timed window / the window's wall "
+                                   "time (k_step, move completions and host work included): a strict lower bound "
+                                   "on the tower's rate")
     if world == 1 and not args.no_cpu_baseline and not args.rehearse:
         tl = time.perf_counter()
         out["cpu_baseline"] = cpu_baseline(args.blocks, args.filters, args.cpu_threads, args.cpu_games,
                                            args.cpu_sims)
         legs["cpu_baseline"] = time.perf_counter() - tl
+        # SURVEY 8d asks for the host's cores: beside the box's 16-thread CPU share, the same sample at
+        # one GPU's share of the host (nproc / 8 on an 8-GPU node)
+        share = max(1, len(os.sched_getaffinity(0)) // 8)
+        if share != args.cpu_threads:
+            tl = time.perf_counter()
+            cb = cpu_baseline(args.blocks, args.filters, share, args.cpu_games, args.cpu_sims, port=False)
+            out["cpu_baseline"]["per_gpu_share"] = {k: cb[k] for k in ("value", "unit", "threads", "sample")}
+            out["cpu_baseline"]["per_gpu_share"]["note"] = "nproc / 8 threads: one GPU's share of an 8-GPU host"
+            legs["cpu_baseline (per-GPU share)"] = time.perf_counter() - tl
     out["legs_wall_s"] = {k: round(v, 2) for k, v in legs.items()}
     out["legs_note"] = "wall time of every leg this run executed (rank 0); only the headline's timed window is `value`"
     print(json.dumps(out))

@@ -236,6 +236,32 @@ def test_winograd_training_convs_match_direct(require_gpu, monkeypatch):
         assert np.linalg.norm(g1[o:o + cnt] - r) <= 1e-2 * max(np.linalg.norm(r), 1e-30), name
 
 
+@pytest.mark.parametrize("fuse", ["1", "0"])
+def test_relu_sign_recompute_is_bit_identical(require_gpu, monkeypatch, fuse):
+    """Round 6 (tr ORC): for a BatchNorm with no residual (BN 0, every block's BN1) the data-grad
+    conv recomputes O > 0 as ((Y - mean) / std) * gamma + beta > 0 -- the forward's own float
+    expression -- instead of reading O, in the BN-backward staging and in the STATS 2 epilogue.
+    Against AZ_TRAIN_ORC=0 (O read from HBM), fused and unfused BN paths: losses, running statistics
+    and every gradient bit-identical, over two steps (the second from the AdamW-updated weights)."""
+    blocks, n = 3, 37
+    w = A.random_weights(blocks, 256, seed=29)
+    planes, tpol, tval = batch(n, seed=501)
+    monkeypatch.setenv("AZ_TRAIN_FUSE_BN", fuse)
+    out = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("AZ_TRAIN_ORC", flag)
+        tr = A.Trainer(blocks, 256, weights=w, max_batch=n)
+        rec = []
+        for it in range(2):
+            rec.append((tr.compute_gradients(planes, tpol, tval), tr.grads(), tr.params()))
+            tr.apply(A.get_cyclical_lr(it))
+        out[flag] = rec
+    for (l1, g1, p1), (l0, g0, p0) in zip(out["1"], out["0"]):
+        assert l1 == l0
+        assert np.array_equal(p1, p0)
+        assert np.array_equal(g1, g0), np.abs(g1 - g0).max()
+
+
 @pytest.mark.parametrize("blocks,n", [(2, 300), (3, 13)])
 def test_bn_staging_matches_separate_bn_kernels(require_gpu, monkeypatch, blocks, n):
     """The BatchNorm apply / backward staged in the Winograd convs (the default) against the same
