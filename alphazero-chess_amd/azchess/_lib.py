@@ -149,6 +149,7 @@ SIGNATURES = [
     ("az_trainer_set_host_reducer", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int]),
     ("az_trainer_set_sharded", C.c_int, [C.c_void_p, C.c_int]),
     ("az_trainer_exchange_stats", C.c_int, [C.c_void_p, P(C.c_int64), P(C.c_int64), P(C.c_double), C.c_int]),
+    ("az_trainer_time_exchanges", C.c_int, [C.c_void_p, C.c_int]),
     ("az_rules_probe", C.c_int, [C.c_int, P(AzPos), P(C.c_int32), C.c_int, P(AzPos), P(C.c_int32), P(C.c_int32),
                                  P(C.c_int32), P(C.c_int32), P(C.c_int32), P(C.c_int32), P(C.c_uint64), P(C.c_float)]),
 ]

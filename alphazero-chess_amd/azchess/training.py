@@ -247,9 +247,13 @@ class Trainer:
         L.check(L.lib.az_trainer_timing(self._h, C.byref(a), C.byref(b), C.byref(n), int(reset)))
         return a.value, b.value, n.value
 
+    def time_exchanges(self, on=True):
+        """HIP events around every exchange of the following steps (for exchange_stats' time)."""
+        L.check(L.lib.az_trainer_time_exchanges(self._h, int(bool(on))))
+
     def exchange_stats(self, reset=False):
         """(collectives, steps, exchange_ms): the data-parallel exchanges since the last reset --
-        how many, over how many applied steps, and their device time."""
+        how many, over how many applied steps, and (while time_exchanges is on) their device time."""
         a, b, c = C.c_int64(), C.c_int64(), C.c_double()
         L.check(L.lib.az_trainer_exchange_stats(self._h, C.byref(a), C.byref(b), C.byref(c), int(reset)))
         return a.value, b.value, c.value

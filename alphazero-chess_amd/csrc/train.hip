@@ -612,6 +612,14 @@ __global__ void bn_local_kernel(const float* __restrict__ part, int nb, int C, i
     if (c == 0) slot[2 * sstride] = (float)R;
 }
 __global__ void set_value_kernel(float* __restrict__ p, float v) { *p = v; }
+// out[i] = sum over ranks r = 0, 1, ... (in order) of slots[r stride + i]
+__global__ void sum_slots_kernel(const float* __restrict__ slots, int world, size_t stride, int n, float* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float s = slots[i];
+    for (int r = 1; r < world; r++) s += slots[(size_t)r * stride + i];
+    out[i] = s;
+}
 // the ranks' slots -> batch mean / std and the running statistics (momentum 0.1, as
 // finalize_var_kernel); nglob (BN 0 only): the global row count for the loss and the BN backward
 // coff: the BatchNorm's first channel in the slots (the two head BatchNorms share one exchange)
@@ -937,7 +945,7 @@ template <bool ADD, int STATS, int XIN, int ORC = 0>
 __global__ void __launch_bounds__(512)
 conv_wino_train_kernel(const float* __restrict__ X, const uint4* __restrict__ U, unsigned ubytes,
                        const float* __restrict__ bias, const float* __restrict__ addend, float* __restrict__ Y,
-                       BoardStats bs, BnIn bn, BnBack bb, int nboards, unsigned long long* trb) {
+                       BoardStats bs, BnIn bn, BnBack bb, int nboards, unsigned long long* trb, int endbar) {
     constexpr int F = 256, NN = WinoCfg<F>::NN, XSn = WinoCfg<F>::XS, PF = WinoCfg<F>::PF, RS = F / 4 + 2;
     constexpr int XSZ = 64 * RS, VSZ = 2 * WinoCfg<F>::CH * 1024 / 16, PAD = WINO_PAD_SQ * RS;
     __shared__ __attribute__((aligned(16))) uint4 lds[PAD + XSZ + PAD + VSZ];
@@ -1108,7 +1116,13 @@ conv_wino_train_kernel(const float* __restrict__ X, const uint4* __restrict__ U,
             }
         }
         wino_stamp(tr, 3);
-        __syncthreads();   // every wave is done with ACT and V before the next board's staging
+        // Round 6: no barrier here.  The next board's staging writes only ACT (dead since the last
+        // chunk's transform, before the chunk barrier every wave passed) and, XIN 2, the bias
+        // partial's scratch at V buffer 0 (dead since that same barrier: the last chunk reads
+        // buffer 1); V itself is written after the staging's barrier, which every wave reaches only
+        // after its epilogue.  So a wave that is done stages its share of the next board while the
+        // others finish their epilogues (endbar = 1: the barrier as before, for A/B).
+        if (endbar) __syncthreads();
     }
 }
 
@@ -1359,7 +1373,8 @@ struct Trainer {
     // loss normalisation over every rank's rows; xfwd [world][2 slot + 1] forward exchange,
     // xback [2 slot] backward exchange, nglob the global row count (device), lossx the losses
     bool sharded = false;
-    float *xfwd = nullptr, *xback = nullptr, *nglob = nullptr, *lossx = nullptr;
+    float *xfwd = nullptr, *xback = nullptr, *xsum = nullptr, *nglob = nullptr, *lossx = nullptr;
+    size_t xbs = 0;                          // floats per rank slot of xback
     int xfwd_world = 0;
     // az_trainer_step in sharded mode: the losses ride in the gradient all-reduce (g[np .. np + 3])
     bool loss_in_grad = false;
@@ -1368,10 +1383,13 @@ struct Trainer {
     // HIP events around each one on the trainer stream (a pool of pairs, summed after each step)
     long long n_exchanges = 0, steps_exchanged = 0;
     double exchange_ms = 0.0;
+    bool xtime = false;                      // events around each exchange (az_trainer_time_exchanges): they
+                                             // cost ~3 us of queue time each, so timing is opt-in
     std::vector<hipEvent_t> xev;
     int xev_used = 0;
     bool fuse_bn = true;                     // BN apply / backward staged in the next Winograd conv (env AZ_TRAIN_FUSE_BN=0: off)
     bool orc = true;                         // O's sign recomputed where no residual (env AZ_TRAIN_ORC=0: off)
+    int endbar = 0;                          // Winograd training convs: barrier between boards (env AZ_TRAIN_ENDBAR=1, A/B)
     // the conv bias gradients of the tower's BatchNorms: bn_back4 partials per BN, summed in one
     // launch at the end of the backward (bias_dst[j] = gradient offset of BN j's conv bias)
     float* bsum_all = nullptr;
@@ -1443,31 +1461,31 @@ int launch_wino(Trainer* T, const float* X, const float* U, const float* bias, c
     // ORC: O's sign recomputed (no residual: BN 0 and BN1s) where the host asks for it
     const int orc = (bb.dy && bb.beta ? 1 : 0) | (stats == 2 && bs.gamma ? 2 : 0);
     if (bn.out)
-        tr::conv_wino_train_kernel<false, 1, 1><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb);
+        tr::conv_wino_train_kernel<false, 1, 1><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb, T->endbar);
     else if (bb.dy && addend && orc == 1)   // conv1's data grad: BN1's backward, BN 2b's statistics
-        tr::conv_wino_train_kernel<true, 2, 2, 1><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, trb);
+        tr::conv_wino_train_kernel<true, 2, 2, 1><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, trb, T->endbar);
     else if (bb.dy && addend && orc == 3)   // ... of block 0 (BN 0 has no residual either)
-        tr::conv_wino_train_kernel<true, 2, 2, 3><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, trb);
+        tr::conv_wino_train_kernel<true, 2, 2, 3><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, trb, T->endbar);
     else if (bb.dy && !addend && orc == 2)  // conv2's data grad: BN2's backward, BN1's statistics
-        tr::conv_wino_train_kernel<false, 2, 2, 2><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb);
+        tr::conv_wino_train_kernel<false, 2, 2, 2><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb, T->endbar);
     else if (bb.dy && addend)
-        tr::conv_wino_train_kernel<true, 2, 2><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, trb);
+        tr::conv_wino_train_kernel<true, 2, 2><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, trb, T->endbar);
     else if (bb.dy)
-        tr::conv_wino_train_kernel<false, 2, 2><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb);
+        tr::conv_wino_train_kernel<false, 2, 2><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb, T->endbar);
     else if (stats == 2 && bs.gamma && addend)   // unfused backward (AZ_TRAIN_FUSE_BN=0), conv1's data grad
-        tr::conv_wino_train_kernel<true, 2, 0, 2><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, trb);
+        tr::conv_wino_train_kernel<true, 2, 0, 2><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, trb, T->endbar);
     else if (stats == 2 && bs.gamma)             // ... conv2's
-        tr::conv_wino_train_kernel<false, 2, 0, 2><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb);
+        tr::conv_wino_train_kernel<false, 2, 0, 2><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb, T->endbar);
     else if (addend && stats == 2)
-        tr::conv_wino_train_kernel<true, 2, 0><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, trb);
+        tr::conv_wino_train_kernel<true, 2, 0><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, trb, T->endbar);
     else if (addend && stats == 0)
-        tr::conv_wino_train_kernel<true, 0, 0><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, trb);
+        tr::conv_wino_train_kernel<true, 0, 0><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, trb, T->endbar);
     else if (!addend && stats == 1)
-        tr::conv_wino_train_kernel<false, 1, 0><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb);
+        tr::conv_wino_train_kernel<false, 1, 0><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb, T->endbar);
     else if (!addend && stats == 2)
-        tr::conv_wino_train_kernel<false, 2, 0><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb);
+        tr::conv_wino_train_kernel<false, 2, 0><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb, T->endbar);
     else if (!addend && stats == 0)
-        tr::conv_wino_train_kernel<false, 0, 0><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb);
+        tr::conv_wino_train_kernel<false, 0, 0><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb, T->endbar);
     else
         return fail("Winograd conv: unsupported statistics mode");
     return hipGetLastError() == hipSuccess ? 0 : fail("Winograd conv launch failed");
@@ -1531,11 +1549,13 @@ int host_allreduce(Trainer* T, float* d, size_t n, const char* what);
 // sum of n floats at d over the ranks, on the trainer stream: RCCL, the host reducer, or nothing
 // (one rank)
 constexpr int XEV_PAIRS = 256;
-int exchange(Trainer* T, float* d, size_t n, const char* what) {
+// one exchange: counted, and bracketed by HIP events while az_trainer_time_exchanges is on
+template <class Fn>
+int exchange_run(Trainer* T, Fn&& fn) {
     if (!T->comm && !T->host_reduce) return 0;
     T->n_exchanges++;
     hipEvent_t* ev = nullptr;   // events around the exchange (none once the pool is used up)
-    if (T->xev_used < XEV_PAIRS) {
+    if (T->xtime && T->xev_used < XEV_PAIRS) {
         if (T->xev.empty()) {
             T->xev.assign(2 * XEV_PAIRS, nullptr);
             for (hipEvent_t& e : T->xev) AZ_HIP(hipEventCreate(&e));
@@ -1543,14 +1563,39 @@ int exchange(Trainer* T, float* d, size_t n, const char* what) {
         ev = &T->xev[2 * T->xev_used++];
         AZ_HIP(hipEventRecord(ev[0], T->st));
     }
-    if (T->comm) {
-        if (ncclAllReduce(d, d, n, ncclFloat, ncclSum, T->comm, T->st) != ncclSuccess)
-            return fail(std::string("ncclAllReduce (") + what + ") failed");
-    } else if (host_allreduce(T, d, n, what)) {
-        return -1;
-    }
+    if (fn() != 0) return -1;
     if (ev) AZ_HIP(hipEventRecord(ev[1], T->st));
     return 0;
+}
+int exchange(Trainer* T, float* d, size_t n, const char* what) {
+    return exchange_run(T, [&]() -> int {
+        if (T->comm) {
+            if (ncclAllReduce(d, d, n, ncclFloat, ncclSum, T->comm, T->st) != ncclSuccess)
+                return fail(std::string("ncclAllReduce (") + what + ") failed");
+            return 0;
+        }
+        return host_allreduce(T, d, n, what);
+    });
+}
+// every rank's slot of n floats, in rank order, into buf[world][n] (this rank's already at
+// buf + rank n): an RCCL all-gather in place (one latency chain of world - 1 hops where an
+// all-reduce takes two), or through the host reducer with the other slots zeroed (x + 0 = x
+// exactly).  Round 6: the sharded BatchNorm exchanges are gathers; whatever is summed over ranks
+// is then summed in rank order on the device (sum_slots_kernel), so RCCL and the host reducer
+// compute the same floats, independent of RCCL's ring / tree order.
+int gather_slots(Trainer* T, float* buf, size_t n, const char* what) {
+    return exchange_run(T, [&]() -> int {
+        if (T->comm) {
+            if (ncclAllGather(buf + (size_t)T->rank * n, buf, n, ncclFloat, T->comm, T->st) != ncclSuccess)
+                return fail(std::string("ncclAllGather (") + what + ") failed");
+            return 0;
+        }
+        if (T->rank > 0) AZ_HIP(hipMemsetAsync(buf, 0, (size_t)T->rank * n * sizeof(float), T->st));
+        if (T->rank + 1 < T->world)
+            AZ_HIP(hipMemsetAsync(buf + (size_t)(T->rank + 1) * n, 0, (size_t)(T->world - 1 - T->rank) * n * sizeof(float),
+                                  T->st));
+        return host_allreduce(T, buf, (size_t)T->world * n, what);
+    });
 }
 // after a step's final synchronisation: the exchanges' device time into exchange_ms
 void exchange_times(Trainer* T) {
@@ -1561,23 +1606,37 @@ void exchange_times(Trainer* T) {
     T->xev_used = 0;
 }
 
-// sharded batch: the exchange buffers for the current world (allocated on first use)
+// sharded batch: the exchange buffers for the current world (allocated on first use):
+// xfwd [world][2 slot + 1] (forward statistics), xback [world][xbs] (backward sums, xbs = 2 slot:
+// the tower's 2F or the heads' 80) + xsum [xbs] (their rank-order sums), nglob, lossx
 int sharded_buffers(Trainer* T) {
     if (T->xfwd && T->xfwd_world == T->world) return 0;
     // every piece 256-byte aligned: the BN backward takes its four-channel path on the exchanged
     // sums exactly when it does on the rank's own (bn_vec), so one rank computes the plain step
-    const size_t nf = ((size_t)T->world * (2 * T->slot + 1) + 63) & ~(size_t)63, nb = ((size_t)2 * T->slot + 63) & ~(size_t)63;
-    float* q = T->alloc(nf + nb + 128);
+    auto up = [](size_t k) { return (k + 63) & ~(size_t)63; };
+    const size_t nf = up((size_t)T->world * (2 * T->slot + 1));
+    T->xbs = up((size_t)2 * T->slot);
+    const size_t nb = (size_t)T->world * T->xbs;
+    float* q = T->alloc(nf + nb + T->xbs + 128);
     if (!q) return fail("sharded batch: out of device memory");
     hipPointerAttribute_t pa;
     if (hipPointerGetAttributes(&pa, q) != hipSuccess || pa.device != T->device)
         return fail("sharded batch: exchange buffers not on the trainer's device");
     T->xfwd = q;
     T->xback = q + nf;
-    T->nglob = T->xback + nb;
+    T->xsum = T->xback + nb;
+    T->nglob = T->xsum + T->xbs;
     T->lossx = T->nglob + 64;
     T->xfwd_world = T->world;
     return 0;
+}
+
+// the backward sums of n floats per rank: this rank's at xback + rank xbs (written by the caller),
+// gathered, summed in rank order into xsum
+int sum_over_ranks(Trainer* T, int n, const char* what) {
+    TRY(gather_slots(T, T->xback, T->xbs, what));
+    tr::sum_slots_kernel<<<(n + 255) / 256, 256, 0, T->st>>>(T->xback, T->world, T->xbs, n, T->xsum);
+    return hipGetLastError() == hipSuccess ? 0 : fail("sum over ranks failed");
 }
 
 // the four-channel BN kernels apply: C a power of two in [4, 1024], ld and every pointer 16-byte
@@ -1619,7 +1678,6 @@ int bn_forward(Trainer* T, int bi, const float* Y, int ld, int C, int R, size_t 
     if (T->sharded) {   // this rank's slot (sum, squared deviations from its mean, rows), exchange, combine
         const int ss = T->slot, rs = 2 * ss + 1;
         float* my = T->xfwd + (size_t)T->rank * rs;
-        AZ_HIP(hipMemsetAsync(T->xfwd, 0, (size_t)T->world * rs * sizeof(float), T->st));
         if (bpart) {
             if (R % 64 || ld != C) return fail("bn: board statistics need whole boards");
             tr::bn_local_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(bpart, R / 64, C, R, my, ss);
@@ -1633,7 +1691,7 @@ int bn_forward(Trainer* T, int bi, const float* Y, int ld, int C, int R, size_t 
                                  {tr::FIN_SUM, my + ss, nullptr, nullptr, nullptr});
             tr::set_value_kernel<<<1, 1, 0, T->st>>>(my + 2 * ss, (float)R);
         }
-        TRY(exchange(T, T->xfwd, (size_t)T->world * rs, "BatchNorm statistics"));
+        TRY(gather_slots(T, T->xfwd, rs, "BatchNorm statistics"));
         tr::bn_global_kernel<<<(C + 255) / 256, 256, 0, T->st>>>(T->xfwd, T->world, C, ss, 0, mean, sd, P + 2 * C,
                                                                  P + 3 * C, bi == 0 ? T->nglob : nullptr);
     } else if (bpart) {
@@ -1660,7 +1718,6 @@ int bn_forward_heads_sharded(Trainer* T, int bi, int R, size_t poff, size_t voff
     const int ss = T->slot, rs = 2 * ss + 1, C = 40;
     float* my = T->xfwd + (size_t)T->rank * rs;
     float* lmean = T->bmean + (size_t)bi * T->slot;   // scratch: this rank's 40 means (the combine overwrites it)
-    AZ_HIP(hipMemsetAsync(T->xfwd, 0, (size_t)T->world * rs * sizeof(float), T->st));
     const int nb = nblk_rows(R);
     dim3 g(nb, 1);
     tr::launch_colsum<0>(g, T->st, T->y40, 64, C, R, nullptr, nullptr, nullptr, nullptr, T->cpart,
@@ -1669,7 +1726,7 @@ int bn_forward_heads_sharded(Trainer* T, int bi, int R, size_t poff, size_t voff
     tr::launch_colsum<1>(g, T->st, T->y40, 64, C, R, lmean, nullptr, nullptr, nullptr, T->cpart,
                          {tr::FIN_SUM, my + ss, nullptr, nullptr, nullptr});
     tr::set_value_kernel<<<1, 1, 0, T->st>>>(my + 2 * ss, (float)R);
-    TRY(exchange(T, T->xfwd, (size_t)T->world * rs, "head BatchNorm statistics"));
+    TRY(gather_slots(T, T->xfwd, rs, "head BatchNorm statistics"));
     float *Pp = T->p + poff, *Pv = T->p + voff;
     tr::bn_global_kernel<<<1, 256, 0, T->st>>>(T->xfwd, T->world, 32, ss, 0, T->bmean + (size_t)bi * ss,
                                                T->bstd + (size_t)bi * ss, Pp + 2 * 32, Pp + 3 * 32, nullptr);
@@ -1711,11 +1768,12 @@ int bn_back_sums(Trainer* T, int bi, const float* dout, const float* O, const fl
     // sharded, the BN backward itself needs the global sums: exchanged through xback
     const float *ug = dgam, *ub = dbet;
     if (T->sharded && xchg) {
-        AZ_HIP(hipMemcpyAsync(T->xback, dbet, C * sizeof(float), hipMemcpyDeviceToDevice, T->st));
-        AZ_HIP(hipMemcpyAsync(T->xback + C, dgam, C * sizeof(float), hipMemcpyDeviceToDevice, T->st));
-        TRY(exchange(T, T->xback, 2 * (size_t)C, "BatchNorm backward sums"));
-        ub = T->xback;
-        ug = T->xback + C;
+        float* my = T->xback + (size_t)T->rank * T->xbs;
+        AZ_HIP(hipMemcpyAsync(my, dbet, C * sizeof(float), hipMemcpyDeviceToDevice, T->st));
+        AZ_HIP(hipMemcpyAsync(my + C, dgam, C * sizeof(float), hipMemcpyDeviceToDevice, T->st));
+        TRY(sum_over_ranks(T, 2 * C, "BatchNorm backward sums"));
+        ub = T->xsum;
+        ug = T->xsum + C;
     }
     *ug_out = ug;
     *ub_out = ub;
@@ -1756,13 +1814,14 @@ int bn_backward_heads_sharded(Trainer* T, int bi, int R, size_t poff, size_t vof
     TRY(bn_back_sums(T, bi + 1, T->da40 + 32, T->a40 + 32, T->y40 + 32, 64, 8, R, voff, nullptr, &ug, &ub, false));
     const size_t off[4] = {poff + 32, poff, voff + 8, voff};      // dbeta_p, dgamma_p, dbeta_v, dgamma_v
     const int pos[4] = {0, 32, 64, 72}, cnt[4] = {32, 32, 8, 8};
+    float* my = T->xback + (size_t)T->rank * T->xbs;
     for (int k = 0; k < 4; k++)
-        AZ_HIP(hipMemcpyAsync(T->xback + pos[k], T->g + off[k], cnt[k] * sizeof(float), hipMemcpyDeviceToDevice, T->st));
-    TRY(exchange(T, T->xback, 80, "head BatchNorm backward sums"));
-    TRY(bn_back_apply(T, bi, T->da40, T->a40, T->y40, 64, 32, R, poff, T->dy40, nullptr, nullptr, T->xback + 32,
-                      T->xback));
+        AZ_HIP(hipMemcpyAsync(my + pos[k], T->g + off[k], cnt[k] * sizeof(float), hipMemcpyDeviceToDevice, T->st));
+    TRY(sum_over_ranks(T, 80, "head BatchNorm backward sums"));
+    TRY(bn_back_apply(T, bi, T->da40, T->a40, T->y40, 64, 32, R, poff, T->dy40, nullptr, nullptr, T->xsum + 32,
+                      T->xsum));
     return bn_back_apply(T, bi + 1, T->da40 + 32, T->a40 + 32, T->y40 + 32, 64, 8, R, voff, T->dy40 + 32, nullptr,
-                         nullptr, T->xback + 72, T->xback + 64);
+                         nullptr, T->xsum + 72, T->xsum + 64);
 }
 
 // the element-wise BN backward with the sums ug (dgamma) / ub (dbeta): dy (+ dres), bias partials
@@ -2204,6 +2263,7 @@ int az_trainer_create(int blocks, int filters, const float* weights, size_t n, i
     ok = ok && hipHostMalloc((void**)&T->hlossx, 4 * sizeof(float), 0) == hipSuccess;
     if (const char* e = getenv("AZ_TRAIN_FUSE_BN")) T->fuse_bn = atoi(e) != 0;
     if (const char* e = getenv("AZ_TRAIN_ORC")) T->orc = atoi(e) != 0;
+    if (const char* e = getenv("AZ_TRAIN_ENDBAR")) T->endbar = atoi(e) != 0;
     if (!ok) { delete T; return fail("az_trainer_create: out of device memory"); }
     // parameters, zero moments, trainable mask (BatchNorm running statistics are not parameters)
     std::vector<uint8_t> mask(T->np, 1);
@@ -2351,6 +2411,12 @@ int az_trainer_set_comm(az_trainer* t, const void* unique_id, int rank, int worl
 int az_trainer_set_sharded(az_trainer* t, int on) {
     if (!t) return fail("null");
     t->t->sharded = on != 0;
+    return 0;
+}
+
+int az_trainer_time_exchanges(az_trainer* t, int on) {
+    if (!t) return fail("null");
+    t->t->xtime = on != 0;
     return 0;
 }
 

@@ -297,9 +297,11 @@ int az_trainer_set_host_reducer(az_trainer* t, az_allreduce_fn fn, void* ctx, in
 int az_trainer_set_sharded(az_trainer* t, int on);
 /* the exchanges of the data-parallel steps since the last reset (RCCL all-reduces or host
  * reductions: sharded BatchNorm statistics and backward sums, losses, gradients, running
- * statistics): how many, over how many applied steps, and their device time (HIP events around
- * each one on the trainer stream) */
+ * statistics): how many, over how many applied steps, and -- while az_trainer_time_exchanges(t, 1)
+ * is on (off by default: the events cost queue time) -- their device time (HIP events around each
+ * one on the trainer stream) */
 int az_trainer_exchange_stats(az_trainer* t, int64_t* collectives, int64_t* steps, double* exchange_ms, int reset);
+int az_trainer_time_exchanges(az_trainer* t, int on);
 
 /* ---- replay buffer: memory.rs ReplayBuffer, host memory ------------ */
 typedef struct az_replay az_replay;

@@ -236,20 +236,24 @@ def test_winograd_training_convs_match_direct(require_gpu, monkeypatch):
         assert np.linalg.norm(g1[o:o + cnt] - r) <= 1e-2 * max(np.linalg.norm(r), 1e-30), name
 
 
-@pytest.mark.parametrize("fuse", ["1", "0"])
-def test_relu_sign_recompute_is_bit_identical(require_gpu, monkeypatch, fuse):
-    """Round 6 (tr ORC): for a BatchNorm with no residual (BN 0, every block's BN1) the data-grad
-    conv recomputes O > 0 as ((Y - mean) / std) * gamma + beta > 0 -- the forward's own float
-    expression -- instead of reading O, in the BN-backward staging and in the STATS 2 epilogue.
-    Against AZ_TRAIN_ORC=0 (O read from HBM), fused and unfused BN paths: losses, running statistics
-    and every gradient bit-identical, over two steps (the second from the AdamW-updated weights)."""
-    blocks, n = 3, 37
+@pytest.mark.parametrize("knob,fuse,n", [("AZ_TRAIN_ORC", "1", 37), ("AZ_TRAIN_ORC", "0", 37),
+                                         ("AZ_TRAIN_ENDBAR", "1", 300)])
+def test_round6_conv_changes_are_bit_identical(require_gpu, monkeypatch, knob, fuse, n):
+    """Round 6, two changes to the persistent Winograd training convs, each against its A/B knob:
+    AZ_TRAIN_ORC -- for a BatchNorm with no residual (BN 0, every block's BN1) the data-grad conv
+    recomputes O > 0 as ((Y - mean) / std) * gamma + beta > 0 (the forward's own float expression)
+    instead of reading O, in the BN-backward staging and in the STATS 2 epilogue (fused and unfused
+    BN paths); AZ_TRAIN_ENDBAR -- no workgroup barrier between a workgroup's boards, so a wave stages
+    the next board while the others finish their epilogues (n = 300: 44 workgroups take two
+    boards).  Losses, running statistics and every gradient bit-identical over two steps (the second
+    from the AdamW-updated weights)."""
+    blocks = 3
     w = A.random_weights(blocks, 256, seed=29)
     planes, tpol, tval = batch(n, seed=501)
     monkeypatch.setenv("AZ_TRAIN_FUSE_BN", fuse)
     out = {}
     for flag in ("1", "0"):
-        monkeypatch.setenv("AZ_TRAIN_ORC", flag)
+        monkeypatch.setenv(knob, flag)
         tr = A.Trainer(blocks, 256, weights=w, max_batch=n)
         rec = []
         for it in range(2):
@@ -446,6 +450,7 @@ def test_sharded_world1_rccl_is_the_plain_step(require_gpu, blocks, filters):
     # az_trainer_step: the losses ride in the gradient all-reduce; the two head BatchNorms share one
     # exchange per direction -> 2 per tower BN + 2 + 1 collectives per step
     b.exchange_stats(reset=True)
+    b.time_exchanges(True)
     for it in range(2, 4):
         la = a.step(planes, tpol, tval, A.get_cyclical_lr(it))
         lb = b.step(planes, tpol, tval, A.get_cyclical_lr(it))
