@@ -60,6 +60,24 @@ def pmc_traffic(games, blocks, filters, dtype, winograd=True):
     return s.get("traffic_bytes"), os.path.relpath(path, ROOT)
 
 
+def cgroup_cpus():
+    """The CPUs the process's cgroup may use (cgroup v2 cpu.max quota / period), or None."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        return None if q == "max" else float(q) / float(p)
+    except (OSError, ValueError):
+        pass
+    try:   # cgroup v1
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = float(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            p = float(f.read())
+        return q / p if q > 0 and p > 0 else None
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(blocks, filters, threads, games, sims, port=True):
     """The reference's self-play on the host cores, a bounded sample of the same workload: `games`
     games from the start position, one move of `sims` simulations each, same 20x256 net (seed 42).
@@ -88,6 +106,7 @@ def cpu_baseline(blocks, filters, threads, games, sims, port=True):
         pass
     out = {"value": nsims / dt, "unit": "sims/s", "kind": "port",
            "cores": os.cpu_count(), "nproc": len(os.sched_getaffinity(0)), "threads": threads,
+           "cpu_quota": cgroup_cpus(),
            "cores_note": "cores = os.cpu_count() of the GPU box's host, nproc = the CPUs this process may run on "
                          "(the box's share), threads = the OpenMP / torch threads the baseline used",
            "cpu_model": model,
@@ -779,7 +798,11 @@ def main():
             tl = time.perf_counter()
             cb = cpu_baseline(args.blocks, args.filters, share, args.cpu_games, args.cpu_sims, port=False)
             out["cpu_baseline"]["per_gpu_share"] = {k: cb[k] for k in ("value", "unit", "threads", "sample")}
-            out["cpu_baseline"]["per_gpu_share"]["note"] = "nproc / 8 threads: one GPU's share of an 8-GPU host"
+            q = cgroup_cpus()
+            out["cpu_baseline"]["per_gpu_share"]["note"] = (
+                "nproc / 8 threads: one GPU's share of an 8-GPU host" +
+                ("; this process's cgroup allows %.0f CPUs, so %d threads oversubscribe it (the 16-thread value "
+                 "above is the box's own share)" % (q, share) if q and q < share else ""))
             legs["cpu_baseline (per-GPU share)"] = time.perf_counter() - tl
     out["legs_wall_s"] = {k: round(v, 2) for k, v in legs.items()}
     out["legs_note"] = "wall time of every leg this run executed (rank 0); only the headline's timed window is `value`"
