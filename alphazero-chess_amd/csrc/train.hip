@@ -945,7 +945,7 @@ template <bool ADD, int STATS, int XIN, int ORC = 0>
 __global__ void __launch_bounds__(512)
 conv_wino_train_kernel(const float* __restrict__ X, const uint4* __restrict__ U, unsigned ubytes,
                        const float* __restrict__ bias, const float* __restrict__ addend, float* __restrict__ Y,
-                       BoardStats bs, BnIn bn, BnBack bb, int nboards, unsigned long long* trb, int endbar) {
+                       BoardStats bs, BnIn bn, BnBack bb, int nboards, unsigned long long* trb) {
     constexpr int F = 256, NN = WinoCfg<F>::NN, XSn = WinoCfg<F>::XS, PF = WinoCfg<F>::PF, RS = F / 4 + 2;
     constexpr int XSZ = 64 * RS, VSZ = 2 * WinoCfg<F>::CH * 1024 / 16, PAD = WINO_PAD_SQ * RS;
     __shared__ __attribute__((aligned(16))) uint4 lds[PAD + XSZ + PAD + VSZ];
@@ -1116,14 +1116,360 @@ conv_wino_train_kernel(const float* __restrict__ X, const uint4* __restrict__ U,
             }
         }
         wino_stamp(tr, 3);
-        // Round 6: no barrier here.  The next board's staging writes only ACT (dead since the last
-        // chunk's transform, before the chunk barrier every wave passed) and, XIN 2, the bias
-        // partial's scratch at V buffer 0 (dead since that same barrier: the last chunk reads
-        // buffer 1); V itself is written after the staging's barrier, which every wave reaches only
-        // after its epilogue.  So a wave that is done stages its share of the next board while the
-        // others finish their epilogues (endbar = 1: the barrier as before, for A/B).
-        if (endbar) __syncthreads();
+        // every wave is done with ACT and V before the next board's staging.  (Round 6: without
+        // this barrier -- legal: the staging writes only ACT and V buffer 0, both dead since the
+        // last chunk's barrier -- a done wave would stage beside the others' epilogues; measured
+        // flat, 22.00-22.10 vs 21.99-22.02 ms per step, profiles/r06d_ab_endbar.txt.)
+        __syncthreads();
     }
+}
+
+// ---------------------------------------------------------------- two workgroups per CU
+// conv_wino_half_kernel: conv_wino_train_kernel's conv, staging and statistics, bit for bit, by two
+// workgroups per board that own half of the output channels each and stream the input through
+// LDS in 16-channel chunks instead of holding the whole board (52 KB of LDS, 4 waves): two
+// workgroups share a CU, so one's staging loads, barriers, epilogue and launch gap run beside the
+// other's MFMAs.  (Phase stamps of the one-board kernel, tools/train_trace.py on MI355X: staging +
+// epilogue + the gap between a CU's boards were 13 % of the forward conv's time and 27 % of the
+// data-grad conv's, with the MFMA core at 88 % of its issue bound.)
+// The price: both halves transform the whole input (a few % of VALU beside the MFMAs) and read it
+// (the second read an L2 hit when the halves run together: both halves of a board go to one XCD).
+// Per chunk k (16 channels, 16 ring steps): the transform of chunk k + 1 (ACT slot (k + 1) & 1 ->
+// V[(k + 1) & 1]) early in the chunk, the staging of chunk k + 2 (global loads at the first step,
+// BatchNorm arithmetic + slot write at the last) into the slot chunk k left, one barrier.
+#ifndef AZ_HALF_ISSUE
+#define AZ_HALF_ISSUE 0   // staging loads of chunk k + 2 at chunk k's first step (1: of chunk k + 3 at its last)
+#endif
+namespace hk {
+constexpr int F = 256, CH = 16, NCH = F / CH, NWV = 4, NN = 2, PF = 2, SPX = 16, LA = 4, TSPLIT = 2;
+constexpr int RS = CH / 4 + 2;                 // uint4 per square in a slot (+2: the patch reads' banks)
+constexpr int R16 = RS * 16, ROW = 8 * R16;    // bytes per square, per board row
+constexpr int SLOT = 64 * RS, PADU = 8 * RS;   // uint4: one chunk of the board, one zero row
+constexpr int XST = CH * 64, VBYTES = CH * 1024;
+constexpr int SLOTS = 3 * PADU + 2 * SLOT;     // [zero row][slot 0][zero row][slot 1][zero row]
+constexpr int PAR = 5 * F / 4;                 // uint4: the staging's per-channel parameters
+constexpr int VB0 = (SLOTS + PAR) * 16;        // bytes: V[2]
+constexpr int LDS_U4 = SLOTS + PAR + 2 * VBYTES / 16;
+__device__ __forceinline__ int slot_off(int s) { return (PADU + s * (SLOT + PADU)) * 16; }
+}  // namespace hk
+
+// one float4 (4 channels of one square) of chunk k per thread: quad tid & 3, square tid >> 2
+template <int XIN> struct HalfStage {
+    float4 a, b, c;
+    size_t e;
+    __device__ __forceinline__ void issue(const float* X, const BnIn& bn, const BnBack& bb, size_t row0, int tid, int k) {
+        e = (row0 + (tid >> 2)) * (hk::F / 4) + 4 * k + (tid & 3);
+        a = reinterpret_cast<const float4*>(X)[e];
+        if constexpr (XIN == 1) {
+            if (bn.res) b = reinterpret_cast<const float4*>(bn.res)[e];
+        } else if constexpr (XIN == 2) {
+            b = reinterpret_cast<const float4*>(bb.O)[e];
+            c = reinterpret_cast<const float4*>(bb.Y)[e];
+        }
+    }
+    // the arithmetic of conv_wino_train_kernel's staging, element for element; the owner of the
+    // chunk writes the activation / dy / dres
+    __device__ __forceinline__ void finish(char* l, const BnIn& bn, const BnBack& bb, float invR, int tid, int k, int s,
+                                           bool owner) const {
+        const int cq = 4 * k + (tid & 3);
+        const float4* par = reinterpret_cast<const float4*>(l + hk::SLOTS * 16);
+        float4 v = a;
+        if constexpr (XIN == 1) {
+            const float4 mu = par[cq], sd = par[64 + cq], ga = par[128 + cq], be = par[192 + cq];
+            const float4 y = a;
+            v = make_float4(((y.x - mu.x) / sd.x) * ga.x + be.x, ((y.y - mu.y) / sd.y) * ga.y + be.y,
+                            ((y.z - mu.z) / sd.z) * ga.z + be.z, ((y.w - mu.w) / sd.w) * ga.w + be.w);
+            if (bn.res) {
+                v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+            }
+            v = make_float4(fmaxf(v.x, 0.0f), fmaxf(v.y, 0.0f), fmaxf(v.z, 0.0f), fmaxf(v.w, 0.0f));
+            if (owner) reinterpret_cast<float4*>(bn.out)[e] = v;
+        } else if constexpr (XIN == 2) {
+            const float4 mu = par[cq], sd = par[64 + cq], ga = par[128 + cq], dg = par[192 + cq], db = par[256 + cq];
+            const float4 d = a, ov = b, y = c;
+            const float4 dz = make_float4(ov.x > 0.0f ? d.x : 0.0f, ov.y > 0.0f ? d.y : 0.0f, ov.z > 0.0f ? d.z : 0.0f,
+                                          ov.w > 0.0f ? d.w : 0.0f);
+            v = make_float4((ga.x / sd.x) * (dz.x - db.x * invR - ((y.x - mu.x) / sd.x) * dg.x * invR),
+                            (ga.y / sd.y) * (dz.y - db.y * invR - ((y.y - mu.y) / sd.y) * dg.y * invR),
+                            (ga.z / sd.z) * (dz.z - db.z * invR - ((y.z - mu.z) / sd.z) * dg.z * invR),
+                            (ga.w / sd.w) * (dz.w - db.w * invR - ((y.w - mu.w) / sd.w) * dg.w * invR));
+            if (owner) {
+                reinterpret_cast<float4*>(bb.dy)[e] = v;
+                if (bb.dres) reinterpret_cast<float4*>(bb.dres)[e] = dz;
+            }
+        }
+        *reinterpret_cast<float4*>(l + hk::slot_off(s) + ((tid >> 2) * hk::RS + (tid & 3)) * 16) = v;
+    }
+};
+
+// the input transform of one chunk from ACT slot s into V[buf]: WinoXf's item (tile row w, tile
+// lane >> 4, channel lane & 15 of the chunk) and arithmetic, over the slot's square stride
+struct HalfXf {
+    char* l;
+    int w, lane;
+    __device__ __forceinline__ void load(int s, f32x2 (&d)[4][2]) const {
+        const int tl = vgpr_index(lane >> 4);
+        const int pc1 = tl * (2 * hk::R16) + (lane & 15) * 4;
+        const int pd0 = tl > 0 ? -hk::R16 : 3 * hk::R16, pd3 = tl < 3 ? 2 * hk::R16 : -2 * hk::R16;
+        const int b1 = hk::slot_off(s) + pc1 + (2 * w - 1) * hk::ROW;
+        const int cb[4] = {b1 + pd0, b1, b1 + hk::R16, b1 + pd3};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const char* p = l + cb[j];
+            d[j][0] = f32x2{*reinterpret_cast<const float*>(p), *reinterpret_cast<const float*>(p + hk::ROW)};
+            d[j][1] = f32x2{*reinterpret_cast<const float*>(p + 2 * hk::ROW), *reinterpret_cast<const float*>(p + 3 * hk::ROW)};
+        }
+    }
+    __device__ __forceinline__ void store(int buf, const f32x2 (&d)[4][2]) const {
+        const int tl = vgpr_index(lane >> 4), tch = lane & 15;
+        const f32x2 m = f32x2{tl > 0 ? 1.0f : 0.0f, tl < 3 ? 1.0f : 0.0f};
+        f32x2 v[4][2];
+        WinoXf<256>::xform(d, m, v);
+        char* vb = l + hk::VB0 + buf * hk::VBYTES + (tch >> 2) * 256 +
+                   (((4 * w + (lane >> 4)) ^ (2 * ((tch >> 2) & 3))) * 16) + (tch & 3) * 4;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+#pragma unroll
+            for (int rp = 0; rp < 2; rp++) {
+                *reinterpret_cast<float*>(vb + ((2 * rp) * 4 + k) * hk::XST) = v[k][rp].x;
+                *reinterpret_cast<float*>(vb + ((2 * rp + 1) * 4 + k) * hk::XST) = v[k][rp].y;
+            }
+    }
+};
+
+// XIN 2: the board's sum of dy over its squares for the 16 channels of the chunk in slot s, in
+// conv_wino_train_kernel's order (row phases r = 0..7 each over squares r + 8 j, then the phases in
+// order); one wave, lane = channel + 16 x phase (r and r + 4)
+__device__ __forceinline__ void half_bsum(const char* l, int s, int lane, float* dst) {
+    const int ch = lane & 15, r4 = lane >> 4;
+    const float* p = reinterpret_cast<const float*>(l + hk::slot_off(s)) + ch;
+    float lo = 0.0f, hi = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        lo += p[(r4 + 8 * j) * hk::RS * 4];
+        hi += p[(r4 + 4 + 8 * j) * hk::RS * 4];
+    }
+    float a = lo;
+#pragma unroll
+    for (int r = 1; r < 8; r++) a += r < 4 ? __shfl(lo, ch + 16 * r, 64) : __shfl(hi, ch + 16 * (r - 4), 64);
+    if (lane < 16) dst[ch] = a;
+}
+
+template <bool ADD, int STATS, int XIN>
+__global__ void __launch_bounds__(256, 2)
+conv_wino_half_kernel(const float* __restrict__ X, const uint4* __restrict__ U, unsigned ubytes,
+                      const float* __restrict__ bias, const float* __restrict__ addend, float* __restrict__ Y,
+                      BoardStats bs, BnIn bn, BnBack bb, int B, unsigned long long* trb) {
+    using namespace hk;
+    __shared__ __attribute__((aligned(16))) uint4 lds[LDS_U4];
+    char* const l = reinterpret_cast<char*>(lds);
+    const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // both halves of a board on one XCD (workgroups go round-robin over the 8 XCDs), one after the other
+    const int bid = blockIdx.x;
+    int board, half;
+    if (B % 8 == 0) {
+        const int j = bid >> 3;
+        half = j & 1;
+        board = (j >> 1) * 8 + (bid & 7);
+    } else {
+        half = bid & 1;
+        board = bid >> 1;
+    }
+    board = vgpr_index(board);
+    const size_t row0 = (size_t)board * 64;
+    const int wg = w + NWV * half;                       // the one-board kernel's wave of these channels
+    unsigned long long* const tr = trb && w == 0 ? trb + (size_t)blockIdx.x * 8 : nullptr;
+    wino_stamp(tr, 0);
+#ifdef AZ_TOWER_TRACE
+    if (tr && lane == 0) {
+        tr[4] = (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));
+        tr[5] = (unsigned)__builtin_amdgcn_s_getreg(20 | (31 << 11));
+    }
+#endif
+    float invR = 0.0f;
+    if constexpr (XIN == 2) invR = 1.0f / (bb.nglob ? bb.nglob[vgpr_index(0)] : (float)bb.R);
+    // zero rows; the staging's parameters
+    for (int c = tid; c < PADU; c += 256)
+#pragma unroll
+        for (int s = 0; s < 3; s++) lds[s * (SLOT + PADU) + c] = make_uint4(0, 0, 0, 0);
+    if constexpr (XIN != 0) {
+        float4* par = reinterpret_cast<float4*>(l + SLOTS * 16);
+        const float* src[5] = {XIN == 1 ? bn.mean : bb.mean, XIN == 1 ? bn.stdv : bb.stdv,
+                               XIN == 1 ? bn.gamma : bb.gamma, XIN == 1 ? bn.beta : bb.dgamma, XIN == 1 ? nullptr : bb.dbeta};
+#pragma unroll
+        for (int p = 0; p < (XIN == 1 ? 4 : 5); p++)
+            if (tid < F / 4) par[64 * p + tid] = reinterpret_cast<const float4*>(src[p])[tid];
+    }
+    __syncthreads();
+    HalfStage<XIN> sg;
+    sg.issue(X, bn, bb, row0, tid, 0);
+    sg.finish(l, bn, bb, invR, tid, 0, 0, half == 0);
+    sg.issue(X, bn, bb, row0, tid, 1);
+    sg.finish(l, bn, bb, invR, tid, 1, 1, half == 1);
+#if AZ_HALF_ISSUE == 1
+    sg.issue(X, bn, bb, row0, tid, 2);
+#endif
+    const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc((void*)U, (short)0, (int)ubytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rN = __builtin_amdgcn_make_buffer_rsrc((void*)U, (short)0, 0, 0x00020000);
+    const int voff = wino_voff<F>(wg, lane);
+    f32x4 wr[PF][NN];
+#pragma unroll
+    for (int i = 0; i < PF; i++)
+#pragma unroll
+        for (int n = 0; n < NN; n++)
+            wr[i][n] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rW, voff + n * 1024, i * 16 * 1024, 0));
+    __syncthreads();
+    const HalfXf xf{l, w, lane};
+    float* const bsd = XIN == 2 ? bb.bsum + (size_t)board * 2 * F : nullptr;
+    {
+        f32x2 d0[4][2];
+        xf.load(0, d0);
+        xf.store(0, d0);
+        if (XIN == 2 && half == 0 && w == 0) half_bsum(l, 0, lane, bsd);
+    }
+    __syncthreads();
+    wino_stamp(tr, 1);
+    const int l16 = lane & 15, h = lane >> 4;
+    const int vrd = h * 256 + ((l16 ^ (2 * h)) * 16);
+    f32x4 acc[16][NN];
+#pragma unroll
+    for (int x = 0; x < 16; x++)
+#pragma unroll
+        for (int n = 0; n < NN; n++) {
+            f32x2 z0, z1;
+            asm volatile("v_mov_b64 %0, 0" : "=v"(z0));
+            asm volatile("v_mov_b64 %0, 0" : "=v"(z1));
+            acc[x][n] = f32x4{z0.x, z0.y, z1.x, z1.y};
+        }
+#pragma unroll 1
+    for (int c = 0; c < NCH; c++) {
+        const int vb = VB0 + (c & 1) * VBYTES + vrd;
+        const bool more = c + 1 < NCH, stg = c + 2 < NCH;
+        f32x2 dn[4][2];
+        f32x4 bq[LA];
+#pragma unroll
+        for (int i = 0; i < LA; i++) bq[i] = *reinterpret_cast<const f32x4*>(l + vb + i * XST);
+#pragma unroll
+        for (int st = 0; st < SPX; st++) {
+            const f32x4 Bf = bq[st % LA];
+            if (st + LA < SPX) bq[st % LA] = *reinterpret_cast<const f32x4*>(l + vb + (st + LA) * XST);
+            f32x4 a[NN];
+#pragma unroll
+            for (int n = 0; n < NN; n++) a[n] = wr[st % PF][n];
+            {
+                const bool nxt = st + PF >= SPX && !more;
+                const int tn = c * SPX + st + PF;
+                const int to = nxt ? tn - NCH * SPX : tn;
+#pragma unroll
+                for (int n = 0; n < NN; n++)
+                    wr[st % PF][n] = __builtin_bit_cast(
+                        f32x4, __builtin_amdgcn_raw_buffer_load_b128(nxt ? rN : rW, voff + n * 1024, WINO_WSTEP(to) * 16 * 1024, 0));
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int s4 = 0; s4 < 4; s4++)
+#pragma unroll
+                for (int n = 0; n < NN; n++)
+                    acc[st][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[n][s4], Bf[s4], acc[st][n], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+#if AZ_HALF_ISSUE == 0
+            if (st == 0 && stg) sg.issue(X, bn, bb, row0, tid, c + 2);
+#endif
+            if (st == 0 && more) xf.load((c + 1) & 1, dn);
+            if (st == TSPLIT && more) {
+                xf.store((c + 1) & 1, dn);
+                if (XIN == 2 && ((c + 1) & 1) == half && w == 0) half_bsum(l, (c + 1) & 1, lane, bsd + (c + 1) * CH);
+            }
+            if (st == SPX - 1 && stg) sg.finish(l, bn, bb, invR, tid, c + 2, c & 1, ((c + 2) & 1) == half);
+#if AZ_HALF_ISSUE == 1
+            // the next staging's loads in flight across the barrier and the next chunk
+            if (st == SPX - 1 && c + 3 < NCH) sg.issue(X, bn, bb, row0, tid, c + 3);
+#endif
+        }
+        if (more) __syncthreads();
+    }
+    wino_stamp(tr, 2);
+    // output transform (wino_core's), then conv_wino_train_kernel's epilogue for these channels
+    const int co0 = wg * 16 * NN + h * 4;
+    f32x4 y[NN][4];
+#pragma unroll
+    for (int n = 0; n < NN; n++) {
+        const f32x4 bb4 = bias ? *reinterpret_cast<const f32x4*>(bias + co0 + n * 16) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int p = 0; p < 2; p++) {
+            f32x2 m[16];
+#pragma unroll
+            for (int x = 0; x < 16; x++) m[x] = p ? f32x2{acc[x][n][2], acc[x][n][3]} : f32x2{acc[x][n][0], acc[x][n][1]};
+            const f32x2 br = p ? f32x2{bb4[2], bb4[3]} : f32x2{bb4[0], bb4[1]};
+            f32x2 s0[4], s1[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                s0[j] = pk_add(pk_add(m[j], m[4 + j]), m[8 + j]);
+                s1[j] = pk_sub(pk_sub(m[4 + j], m[8 + j]), m[12 + j]);
+            }
+            const f32x2 q0 = pk_add(pk_add(pk_add(s0[0], s0[1]), s0[2]), br);
+            const f32x2 q1 = pk_add(pk_sub(pk_sub(s0[1], s0[2]), s0[3]), br);
+            const f32x2 q2 = pk_add(pk_add(pk_add(s1[0], s1[1]), s1[2]), br);
+            const f32x2 q3 = pk_add(pk_sub(pk_sub(s1[1], s1[2]), s1[3]), br);
+            y[n][0][2 * p] = q0.x; y[n][0][2 * p + 1] = q0.y;
+            y[n][1][2 * p] = q1.x; y[n][1][2 * p + 1] = q1.y;
+            y[n][2][2 * p] = q2.x; y[n][2][2 * p + 1] = q2.y;
+            y[n][3][2 * p] = q3.x; y[n][3][2 * p + 1] = q3.y;
+        }
+    }
+    const int ty = l16 >> 2, tx = l16 & 3;
+    f32x4 s0[NN], s1[NN];
+#pragma unroll
+    for (int n = 0; n < NN; n++) {
+        s0[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+        s1[n] = s0[n];
+        f32x4 mu = s0[n], sd = s0[n];
+        if constexpr (STATS == 2) {
+            mu = *reinterpret_cast<const f32x4*>(bs.mean + co0 + n * 16);
+            sd = *reinterpret_cast<const f32x4*>(bs.stdv + co0 + n * 16);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const size_t o = (row0 + (2 * ty + (q >> 1)) * 8 + 2 * tx + (q & 1)) * F + co0 + n * 16;
+            f32x4 v = y[n][q];
+            if constexpr (ADD) v += *reinterpret_cast<const f32x4*>(addend + o);
+            *reinterpret_cast<f32x4*>(Y + o) = v;
+            if constexpr (STATS == 1) {
+                y[n][q] = v;
+                s0[n] += v;
+            } else if constexpr (STATS == 2) {
+                const f32x4 ov = *reinterpret_cast<const f32x4*>(bs.O + o);
+                const f32x4 yb = *reinterpret_cast<const f32x4*>(bs.Ybn + o);
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const float dz = ov[r] > 0.0f ? v[r] : 0.0f;
+                    s0[n][r] += dz;
+                    s1[n][r] += dz * ((yb[r] - mu[r]) / sd[r]);
+                }
+            }
+        }
+    }
+    if constexpr (STATS != 0) {
+#pragma unroll
+        for (int n = 0; n < NN; n++) {
+            s0[n] = sum16(s0[n]);
+            if constexpr (STATS == 1) {
+                const f32x4 mb = s0[n] / 64.0f;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const f32x4 d = y[n][q] - mb;
+                    s1[n] += d * d;
+                }
+            }
+            s1[n] = sum16(s1[n]);
+            if (l16 == 0) {
+                float* pb = bs.part + (size_t)board * 2 * F + co0 + n * 16;
+                *reinterpret_cast<f32x4*>(pb) = s0[n];
+                *reinterpret_cast<f32x4*>(pb + F) = s1[n];
+            }
+        }
+    }
+    wino_stamp(tr, 3);
 }
 
 // Winograd weights U = G g G^T (f64, rounded once to f32: the same arithmetic as net.hip's
@@ -1389,7 +1735,7 @@ struct Trainer {
     int xev_used = 0;
     bool fuse_bn = true;                     // BN apply / backward staged in the next Winograd conv (env AZ_TRAIN_FUSE_BN=0: off)
     bool orc = true;                         // O's sign recomputed where no residual (env AZ_TRAIN_ORC=0: off)
-    int endbar = 0;                          // Winograd training convs: barrier between boards (env AZ_TRAIN_ENDBAR=1, A/B)
+    int half = -1;                           // half-channel conv workgroups: -1 when 2B <= the CU count, 0 never, 1 always (env AZ_TRAIN_HALF)
     // the conv bias gradients of the tower's BatchNorms: bn_back4 partials per BN, summed in one
     // launch at the end of the backward (bias_dst[j] = gradient offset of BN j's conv bias)
     float* bsum_all = nullptr;
@@ -1457,35 +1803,59 @@ int launch_wino(Trainer* T, const float* X, const float* U, const float* bias, c
         trb = g_trace + (size_t)(g_trace_n++ % TRACE_LAUNCHES) * TRACE_BOARDS * 8;
     }
 #endif
+    // small batches (the 512 / world shard of a sharded step): two half-channel workgroups per board
+    // fill twice the CUs (conv_wino_half_kernel, bit-identical to the one-board kernel)
+    if (T->half > 0 || (T->half < 0 && 2 * B <= AZ_TRAIN_WG)) {
+        unsigned long long* htr = nullptr;
+        if (bn.out)
+            tr::conv_wino_half_kernel<false, 1, 1><<<2 * B, 256, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, htr);
+        else if (bb.dy && addend)
+            tr::conv_wino_half_kernel<true, 2, 2><<<2 * B, 256, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, htr);
+        else if (bb.dy)
+            tr::conv_wino_half_kernel<false, 2, 2><<<2 * B, 256, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, htr);
+        else if (addend && stats == 2)
+            tr::conv_wino_half_kernel<true, 2, 0><<<2 * B, 256, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, htr);
+        else if (addend && stats == 0)
+            tr::conv_wino_half_kernel<true, 0, 0><<<2 * B, 256, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, htr);
+        else if (!addend && stats == 1)
+            tr::conv_wino_half_kernel<false, 1, 0><<<2 * B, 256, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, htr);
+        else if (!addend && stats == 2)
+            tr::conv_wino_half_kernel<false, 2, 0><<<2 * B, 256, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, htr);
+        else if (!addend && stats == 0)
+            tr::conv_wino_half_kernel<false, 0, 0><<<2 * B, 256, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, htr);
+        else
+            return fail("Winograd conv: unsupported statistics mode");
+        return hipGetLastError() == hipSuccess ? 0 : fail("Winograd conv launch failed");
+    }
     const unsigned wg = (unsigned)std::min(B, AZ_TRAIN_WG);   // persistent workgroups (one per CU)
     // ORC: O's sign recomputed (no residual: BN 0 and BN1s) where the host asks for it
     const int orc = (bb.dy && bb.beta ? 1 : 0) | (stats == 2 && bs.gamma ? 2 : 0);
     if (bn.out)
-        tr::conv_wino_train_kernel<false, 1, 1><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb, T->endbar);
+        tr::conv_wino_train_kernel<false, 1, 1><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb);
     else if (bb.dy && addend && orc == 1)   // conv1's data grad: BN1's backward, BN 2b's statistics
-        tr::conv_wino_train_kernel<true, 2, 2, 1><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, trb, T->endbar);
+        tr::conv_wino_train_kernel<true, 2, 2, 1><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, trb);
     else if (bb.dy && addend && orc == 3)   // ... of block 0 (BN 0 has no residual either)
-        tr::conv_wino_train_kernel<true, 2, 2, 3><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, trb, T->endbar);
+        tr::conv_wino_train_kernel<true, 2, 2, 3><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, trb);
     else if (bb.dy && !addend && orc == 2)  // conv2's data grad: BN2's backward, BN1's statistics
-        tr::conv_wino_train_kernel<false, 2, 2, 2><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb, T->endbar);
+        tr::conv_wino_train_kernel<false, 2, 2, 2><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb);
     else if (bb.dy && addend)
-        tr::conv_wino_train_kernel<true, 2, 2><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, trb, T->endbar);
+        tr::conv_wino_train_kernel<true, 2, 2><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, trb);
     else if (bb.dy)
-        tr::conv_wino_train_kernel<false, 2, 2><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb, T->endbar);
+        tr::conv_wino_train_kernel<false, 2, 2><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb);
     else if (stats == 2 && bs.gamma && addend)   // unfused backward (AZ_TRAIN_FUSE_BN=0), conv1's data grad
-        tr::conv_wino_train_kernel<true, 2, 0, 2><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, trb, T->endbar);
+        tr::conv_wino_train_kernel<true, 2, 0, 2><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, trb);
     else if (stats == 2 && bs.gamma)             // ... conv2's
-        tr::conv_wino_train_kernel<false, 2, 0, 2><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb, T->endbar);
+        tr::conv_wino_train_kernel<false, 2, 0, 2><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb);
     else if (addend && stats == 2)
-        tr::conv_wino_train_kernel<true, 2, 0><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, trb, T->endbar);
+        tr::conv_wino_train_kernel<true, 2, 0><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, trb);
     else if (addend && stats == 0)
-        tr::conv_wino_train_kernel<true, 0, 0><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, trb, T->endbar);
+        tr::conv_wino_train_kernel<true, 0, 0><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, trb);
     else if (!addend && stats == 1)
-        tr::conv_wino_train_kernel<false, 1, 0><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb, T->endbar);
+        tr::conv_wino_train_kernel<false, 1, 0><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb);
     else if (!addend && stats == 2)
-        tr::conv_wino_train_kernel<false, 2, 0><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb, T->endbar);
+        tr::conv_wino_train_kernel<false, 2, 0><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb);
     else if (!addend && stats == 0)
-        tr::conv_wino_train_kernel<false, 0, 0><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb, T->endbar);
+        tr::conv_wino_train_kernel<false, 0, 0><<<wg, 512, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, trb);
     else
         return fail("Winograd conv: unsupported statistics mode");
     return hipGetLastError() == hipSuccess ? 0 : fail("Winograd conv launch failed");
@@ -2263,7 +2633,7 @@ int az_trainer_create(int blocks, int filters, const float* weights, size_t n, i
     ok = ok && hipHostMalloc((void**)&T->hlossx, 4 * sizeof(float), 0) == hipSuccess;
     if (const char* e = getenv("AZ_TRAIN_FUSE_BN")) T->fuse_bn = atoi(e) != 0;
     if (const char* e = getenv("AZ_TRAIN_ORC")) T->orc = atoi(e) != 0;
-    if (const char* e = getenv("AZ_TRAIN_ENDBAR")) T->endbar = atoi(e) != 0;
+    if (const char* e = getenv("AZ_TRAIN_HALF")) T->half = atoi(e);
     if (!ok) { delete T; return fail("az_trainer_create: out of device memory"); }
     // parameters, zero moments, trainable mask (BatchNorm running statistics are not parameters)
     std::vector<uint8_t> mask(T->np, 1);

@@ -236,17 +236,14 @@ def test_winograd_training_convs_match_direct(require_gpu, monkeypatch):
         assert np.linalg.norm(g1[o:o + cnt] - r) <= 1e-2 * max(np.linalg.norm(r), 1e-30), name
 
 
-@pytest.mark.parametrize("knob,fuse,n", [("AZ_TRAIN_ORC", "1", 37), ("AZ_TRAIN_ORC", "0", 37),
-                                         ("AZ_TRAIN_ENDBAR", "1", 300)])
+@pytest.mark.parametrize("knob,fuse,n", [("AZ_TRAIN_ORC", "1", 300), ("AZ_TRAIN_ORC", "0", 37)])
 def test_round6_conv_changes_are_bit_identical(require_gpu, monkeypatch, knob, fuse, n):
-    """Round 6, two changes to the persistent Winograd training convs, each against its A/B knob:
-    AZ_TRAIN_ORC -- for a BatchNorm with no residual (BN 0, every block's BN1) the data-grad conv
-    recomputes O > 0 as ((Y - mean) / std) * gamma + beta > 0 (the forward's own float expression)
-    instead of reading O, in the BN-backward staging and in the STATS 2 epilogue (fused and unfused
-    BN paths); AZ_TRAIN_ENDBAR -- no workgroup barrier between a workgroup's boards, so a wave stages
-    the next board while the others finish their epilogues (n = 300: 44 workgroups take two
-    boards).  Losses, running statistics and every gradient bit-identical over two steps (the second
-    from the AdamW-updated weights)."""
+    """Round 6, AZ_TRAIN_ORC: for a BatchNorm with no residual (BN 0, every block's BN1) the data-grad
+    conv recomputes O > 0 as ((Y - mean) / std) * gamma + beta > 0 (the forward's own float
+    expression) instead of reading O, in the BN-backward staging and in the STATS 2 epilogue (fused
+    and unfused BN paths; n = 300: the persistent one-board kernel, 44 workgroups take two boards;
+    n = 37: the half-channel kernel, which reads O either way).  Losses, running statistics and
+    every gradient bit-identical over two steps (the second from the AdamW-updated weights)."""
     blocks = 3
     w = A.random_weights(blocks, 256, seed=29)
     planes, tpol, tval = batch(n, seed=501)
@@ -298,6 +295,30 @@ def test_bn_staging_matches_separate_bn_kernels(require_gpu, monkeypatch, blocks
         assert np.array_equal(a, b), (name, np.abs(a - b).max())
         checked += 1
     assert checked > 4 * blocks
+
+
+@pytest.mark.parametrize("blocks,n,fuse", [(20, 4, "1"), (2, 80, "1"), (2, 80, "0"), (3, 13, "0"), (2, 128, "1")])
+def test_half_workgroup_convs_bit_identical(require_gpu, monkeypatch, blocks, n, fuse):
+    """Round 6: at small batches (2 B <= 256, the 512 / world shard of a sharded step at world >= 4)
+    the Winograd convs run as two half-channel workgroups per board (conv_wino_half_kernel, so
+    twice the CUs work); against the persistent one-board kernel (AZ_TRAIN_HALF=0): the same MFMA
+    accumulation order, transforms, BatchNorm staging and per-board statistics, so two steps give
+    bit-identical losses, gradients and parameters.  n = 80 / 128 map both halves of a board to one
+    XCD (n % 8 == 0), n = 4 / 13 take the plain board order; fuse = "0" runs the convs without
+    BatchNorm staging (AZ_TRAIN_FUSE_BN=0)."""
+    w = A.random_weights(blocks, 256, seed=17)
+    planes, tpol, tval = batch(n, seed=300 + n)
+    monkeypatch.setenv("AZ_TRAIN_FUSE_BN", fuse)
+    out = {}
+    for flag in ("-1", "0"):
+        monkeypatch.setenv("AZ_TRAIN_HALF", flag)
+        tr = A.Trainer(blocks, 256, weights=w, max_batch=n)
+        losses = [tr.step(planes, tpol, tval, A.get_cyclical_lr(it)) for it in range(2)]
+        out[flag] = (losses, tr.grads(), tr.params())
+    (l1, g1, p1), (l0, g0, p0) = out["-1"], out["0"]
+    assert l1 == l0
+    assert np.array_equal(g1, g0), np.abs(g1 - g0).max()
+    assert np.array_equal(p1, p0), np.abs(p1 - p0).max()
 
 
 def test_winograd_weight_grad_multi_split(require_gpu):
