@@ -1,5 +1,5 @@
 """A few training steps (training.rs:147-190) at 20x256, batch 512, for rocprofv3 kernel stats.
-Usage: python tools/train_prof.py [steps]"""
+Usage: python tools/train_prof.py [steps] [batch]"""
 import os
 import sys
 import time
@@ -9,7 +9,7 @@ import numpy as np
 import azchess as A
 
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-B = 512
+B = int(sys.argv[2]) if len(sys.argv) > 2 else 512
 rng = np.random.default_rng(1)
 planes = (rng.random((B, 19, 64)) < 0.1).astype(np.float32)
 pol = rng.random((B, 4096)).astype(np.float32)
