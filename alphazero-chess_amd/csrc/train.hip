@@ -1141,7 +1141,7 @@ conv_wino_train_kernel(const float* __restrict__ X, const uint4* __restrict__ U,
 #define AZ_HALF_ISSUE 0   // staging loads of chunk k + 2 at chunk k's first step (1: of chunk k + 3 at its last)
 #endif
 namespace hk {
-constexpr int F = 256, CH = 16, NCH = F / CH, NWV = 4, NN = 2, PF = 2, SPX = 16, LA = 4, TSPLIT = 2;
+constexpr int F = 256, CH = 16, NCH = F / CH, NWV = 4, PF = 2, SPX = 16, LA = 4, TSPLIT = 2;
 constexpr int RS = CH / 4 + 2;                 // uint4 per square in a slot (+2: the patch reads' banks)
 constexpr int R16 = RS * 16, ROW = 8 * R16;    // bytes per square, per board row
 constexpr int SLOT = 64 * RS, PADU = 8 * RS;   // uint4: one chunk of the board, one zero row
@@ -1255,29 +1255,35 @@ __device__ __forceinline__ void half_bsum(const char* l, int s, int lane, float*
     if (lane < 16) dst[ch] = a;
 }
 
-template <bool ADD, int STATS, int XIN>
+// NP = 2 (halves) or 4 (quarters: 256 workgroups at 64 boards, one wave per SIMD of 16 output
+// channels, two steps' MFMAs interleaved so that two independent accumulator chains hide the f32
+// MFMA's dependent latency; every accumulator still takes its MFMAs in the same order)
+template <int NP, bool ADD, int STATS, int XIN>
 __global__ void __launch_bounds__(256, 2)
-conv_wino_half_kernel(const float* __restrict__ X, const uint4* __restrict__ U, unsigned ubytes,
+conv_wino_part_kernel(const float* __restrict__ X, const uint4* __restrict__ U, unsigned ubytes,
                       const float* __restrict__ bias, const float* __restrict__ addend, float* __restrict__ Y,
                       BoardStats bs, BnIn bn, BnBack bb, int B, unsigned long long* trb) {
     using namespace hk;
+    constexpr int NB = 16 / (NP * NWV);                  // 16-channel output blocks per wave
+    constexpr int SPI = NB == 1 ? 2 : 1;                 // ring steps per MFMA group
+    static_assert(NB * NP * NWV == 16 && SPX % SPI == 0, "part kernel config");
     __shared__ __attribute__((aligned(16))) uint4 lds[LDS_U4];
     char* const l = reinterpret_cast<char*>(lds);
     const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    // both halves of a board on one XCD (workgroups go round-robin over the 8 XCDs), one after the other
+    // all parts of a board on one XCD (workgroups go round-robin over the 8 XCDs), one after the other
     const int bid = blockIdx.x;
-    int board, half;
+    int board, part;
     if (B % 8 == 0) {
         const int j = bid >> 3;
-        half = j & 1;
-        board = (j >> 1) * 8 + (bid & 7);
+        part = j % NP;
+        board = (j / NP) * 8 + (bid & 7);
     } else {
-        half = bid & 1;
-        board = bid >> 1;
+        part = bid % NP;
+        board = bid / NP;
     }
     board = vgpr_index(board);
     const size_t row0 = (size_t)board * 64;
-    const int wg = w + NWV * half;                       // the one-board kernel's wave of these channels
+    const int cb0 = (part * NWV + w) * NB;               // this wave's first 16-channel output block
     unsigned long long* const tr = trb && w == 0 ? trb + (size_t)blockIdx.x * 8 : nullptr;
     wino_stamp(tr, 0);
 #ifdef AZ_TOWER_TRACE
@@ -1303,20 +1309,20 @@ conv_wino_half_kernel(const float* __restrict__ X, const uint4* __restrict__ U, 
     __syncthreads();
     HalfStage<XIN> sg;
     sg.issue(X, bn, bb, row0, tid, 0);
-    sg.finish(l, bn, bb, invR, tid, 0, 0, half == 0);
+    sg.finish(l, bn, bb, invR, tid, 0, 0, part == 0);
     sg.issue(X, bn, bb, row0, tid, 1);
-    sg.finish(l, bn, bb, invR, tid, 1, 1, half == 1);
+    sg.finish(l, bn, bb, invR, tid, 1, 1, part == 1 % NP);
 #if AZ_HALF_ISSUE == 1
     sg.issue(X, bn, bb, row0, tid, 2);
 #endif
     const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc((void*)U, (short)0, (int)ubytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rN = __builtin_amdgcn_make_buffer_rsrc((void*)U, (short)0, 0, 0x00020000);
-    const int voff = wino_voff<F>(wg, lane);
-    f32x4 wr[PF][NN];
+    const int voff = (cb0 * 64 + lane) * 16;           // wino_voff: fragment (block, lane)
+    f32x4 wr[PF][NB];
 #pragma unroll
     for (int i = 0; i < PF; i++)
 #pragma unroll
-        for (int n = 0; n < NN; n++)
+        for (int n = 0; n < NB; n++)
             wr[i][n] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rW, voff + n * 1024, i * 16 * 1024, 0));
     __syncthreads();
     const HalfXf xf{l, w, lane};
@@ -1325,17 +1331,17 @@ conv_wino_half_kernel(const float* __restrict__ X, const uint4* __restrict__ U, 
         f32x2 d0[4][2];
         xf.load(0, d0);
         xf.store(0, d0);
-        if (XIN == 2 && half == 0 && w == 0) half_bsum(l, 0, lane, bsd);
+        if (XIN == 2 && part == 0 && w == 0) half_bsum(l, 0, lane, bsd);
     }
     __syncthreads();
     wino_stamp(tr, 1);
     const int l16 = lane & 15, h = lane >> 4;
     const int vrd = h * 256 + ((l16 ^ (2 * h)) * 16);
-    f32x4 acc[16][NN];
+    f32x4 acc[16][NB];
 #pragma unroll
     for (int x = 0; x < 16; x++)
 #pragma unroll
-        for (int n = 0; n < NN; n++) {
+        for (int n = 0; n < NB; n++) {
             f32x2 z0, z1;
             asm volatile("v_mov_b64 %0, 0" : "=v"(z0));
             asm volatile("v_mov_b64 %0, 0" : "=v"(z1));
@@ -1350,18 +1356,20 @@ conv_wino_half_kernel(const float* __restrict__ X, const uint4* __restrict__ U, 
 #pragma unroll
         for (int i = 0; i < LA; i++) bq[i] = *reinterpret_cast<const f32x4*>(l + vb + i * XST);
 #pragma unroll
-        for (int st = 0; st < SPX; st++) {
-            const f32x4 Bf = bq[st % LA];
-            if (st + LA < SPX) bq[st % LA] = *reinterpret_cast<const f32x4*>(l + vb + (st + LA) * XST);
-            f32x4 a[NN];
+        for (int s0t = 0; s0t < SPX; s0t += SPI) {
+            f32x4 Bf[SPI], a[SPI][NB];
 #pragma unroll
-            for (int n = 0; n < NN; n++) a[n] = wr[st % PF][n];
-            {
+            for (int u = 0; u < SPI; u++) {
+                const int st = s0t + u;
+                Bf[u] = bq[st % LA];
+                if (st + LA < SPX) bq[st % LA] = *reinterpret_cast<const f32x4*>(l + vb + (st + LA) * XST);
+#pragma unroll
+                for (int n = 0; n < NB; n++) a[u][n] = wr[st % PF][n];
                 const bool nxt = st + PF >= SPX && !more;
                 const int tn = c * SPX + st + PF;
                 const int to = nxt ? tn - NCH * SPX : tn;
 #pragma unroll
-                for (int n = 0; n < NN; n++)
+                for (int n = 0; n < NB; n++)
                     wr[st % PF][n] = __builtin_bit_cast(
                         f32x4, __builtin_amdgcn_raw_buffer_load_b128(nxt ? rN : rW, voff + n * 1024, WINO_WSTEP(to) * 16 * 1024, 0));
             }
@@ -1369,31 +1377,37 @@ conv_wino_half_kernel(const float* __restrict__ X, const uint4* __restrict__ U, 
 #pragma unroll
             for (int s4 = 0; s4 < 4; s4++)
 #pragma unroll
-                for (int n = 0; n < NN; n++)
-                    acc[st][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[n][s4], Bf[s4], acc[st][n], 0, 0, 0);
+                for (int u = 0; u < SPI; u++)
+#pragma unroll
+                    for (int n = 0; n < NB; n++)
+                        acc[s0t + u][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][n][s4], Bf[u][s4], acc[s0t + u][n], 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < SPI; u++) {
+                const int st = s0t + u;
 #if AZ_HALF_ISSUE == 0
-            if (st == 0 && stg) sg.issue(X, bn, bb, row0, tid, c + 2);
+                if (st == 0 && stg) sg.issue(X, bn, bb, row0, tid, c + 2);
 #endif
-            if (st == 0 && more) xf.load((c + 1) & 1, dn);
-            if (st == TSPLIT && more) {
-                xf.store((c + 1) & 1, dn);
-                if (XIN == 2 && ((c + 1) & 1) == half && w == 0) half_bsum(l, (c + 1) & 1, lane, bsd + (c + 1) * CH);
-            }
-            if (st == SPX - 1 && stg) sg.finish(l, bn, bb, invR, tid, c + 2, c & 1, ((c + 2) & 1) == half);
+                if (st == 0 && more) xf.load((c + 1) & 1, dn);
+                if (st == TSPLIT && more) {
+                    xf.store((c + 1) & 1, dn);
+                    if (XIN == 2 && (c + 1) % NP == part && w == 0) half_bsum(l, (c + 1) & 1, lane, bsd + (c + 1) * CH);
+                }
+                if (st == SPX - 1 && stg) sg.finish(l, bn, bb, invR, tid, c + 2, c & 1, (c + 2) % NP == part);
 #if AZ_HALF_ISSUE == 1
-            // the next staging's loads in flight across the barrier and the next chunk
-            if (st == SPX - 1 && c + 3 < NCH) sg.issue(X, bn, bb, row0, tid, c + 3);
+                // the next staging's loads in flight across the barrier and the next chunk
+                if (st == SPX - 1 && c + 3 < NCH) sg.issue(X, bn, bb, row0, tid, c + 3);
 #endif
+            }
         }
         if (more) __syncthreads();
     }
     wino_stamp(tr, 2);
     // output transform (wino_core's), then conv_wino_train_kernel's epilogue for these channels
-    const int co0 = wg * 16 * NN + h * 4;
-    f32x4 y[NN][4];
+    const int co0 = cb0 * 16 + h * 4;
+    f32x4 y[NB][4];
 #pragma unroll
-    for (int n = 0; n < NN; n++) {
+    for (int n = 0; n < NB; n++) {
         const f32x4 bb4 = bias ? *reinterpret_cast<const f32x4*>(bias + co0 + n * 16) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int p = 0; p < 2; p++) {
@@ -1418,9 +1432,9 @@ conv_wino_half_kernel(const float* __restrict__ X, const uint4* __restrict__ U, 
         }
     }
     const int ty = l16 >> 2, tx = l16 & 3;
-    f32x4 s0[NN], s1[NN];
+    f32x4 s0[NB], s1[NB];
 #pragma unroll
-    for (int n = 0; n < NN; n++) {
+    for (int n = 0; n < NB; n++) {
         s0[n] = f32x4{0.f, 0.f, 0.f, 0.f};
         s1[n] = s0[n];
         f32x4 mu = s0[n], sd = s0[n];
@@ -1451,7 +1465,7 @@ conv_wino_half_kernel(const float* __restrict__ X, const uint4* __restrict__ U, 
     }
     if constexpr (STATS != 0) {
 #pragma unroll
-        for (int n = 0; n < NN; n++) {
+        for (int n = 0; n < NB; n++) {
             s0[n] = sum16(s0[n]);
             if constexpr (STATS == 1) {
                 const f32x4 mb = s0[n] / 64.0f;
@@ -1735,7 +1749,8 @@ struct Trainer {
     int xev_used = 0;
     bool fuse_bn = true;                     // BN apply / backward staged in the next Winograd conv (env AZ_TRAIN_FUSE_BN=0: off)
     bool orc = true;                         // O's sign recomputed where no residual (env AZ_TRAIN_ORC=0: off)
-    int half = -1;                           // half-channel conv workgroups: -1 when 2B <= the CU count, 0 never, 1 always (env AZ_TRAIN_HALF)
+    int half = -1;                           // conv workgroups per board at small batches: -1 auto (4 when 4B <= the CU
+                                             // count, 2 when 2B <=), 0 one per board, 2 / 4 always (env AZ_TRAIN_HALF)
     // the conv bias gradients of the tower's BatchNorms: bn_back4 partials per BN, summed in one
     // launch at the end of the backward (bias_dst[j] = gradient offset of BN j's conv bias)
     float* bsum_all = nullptr;
@@ -1783,6 +1798,33 @@ int launch_conv(Trainer* T, int taps, const float* X, int ldx, int K, const floa
     return hipGetLastError() == hipSuccess ? 0 : fail("conv launch failed");
 }
 
+// the part kernel (NP workgroups per board) of launch_wino
+template <int NPART>
+int launch_wino_part(Trainer* T, const float* X, const uint4* U4, unsigned ub, const float* bias, const float* addend,
+                     float* Y, int B, int stats, tr::BoardStats bs, tr::BnIn bn, tr::BnBack bb) {
+    unsigned long long* htr = nullptr;
+    const unsigned g = (unsigned)(NPART * B);
+    if (bn.out)
+        tr::conv_wino_part_kernel<NPART, false, 1, 1><<<g, 256, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, htr);
+    else if (bb.dy && addend)
+        tr::conv_wino_part_kernel<NPART, true, 2, 2><<<g, 256, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, htr);
+    else if (bb.dy)
+        tr::conv_wino_part_kernel<NPART, false, 2, 2><<<g, 256, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, htr);
+    else if (addend && stats == 2)
+        tr::conv_wino_part_kernel<NPART, true, 2, 0><<<g, 256, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, htr);
+    else if (addend && stats == 0)
+        tr::conv_wino_part_kernel<NPART, true, 0, 0><<<g, 256, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, htr);
+    else if (!addend && stats == 1)
+        tr::conv_wino_part_kernel<NPART, false, 1, 0><<<g, 256, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, htr);
+    else if (!addend && stats == 2)
+        tr::conv_wino_part_kernel<NPART, false, 2, 0><<<g, 256, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, htr);
+    else if (!addend && stats == 0)
+        tr::conv_wino_part_kernel<NPART, false, 0, 0><<<g, 256, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, htr);
+    else
+        return fail("Winograd conv: unsupported statistics mode");
+    return hipGetLastError() == hipSuccess ? 0 : fail("Winograd conv launch failed");
+}
+
 // Y = conv3x3(X, U) (+ bias) (+ addend) over B whole boards, Winograd (F = 256 residual convs);
 // stats 1 / 2: per-board BN partials into bs.part (tr::BoardStats)
 // bn.out non-null: X is the previous conv's pre-BN output, BatchNorm + ReLU (+ bn.res) applied in
@@ -1803,30 +1845,13 @@ int launch_wino(Trainer* T, const float* X, const float* U, const float* bias, c
         trb = g_trace + (size_t)(g_trace_n++ % TRACE_LAUNCHES) * TRACE_BOARDS * 8;
     }
 #endif
-    // small batches (the 512 / world shard of a sharded step): two half-channel workgroups per board
-    // fill twice the CUs (conv_wino_half_kernel, bit-identical to the one-board kernel)
-    if (T->half > 0 || (T->half < 0 && 2 * B <= AZ_TRAIN_WG)) {
-        unsigned long long* htr = nullptr;
-        if (bn.out)
-            tr::conv_wino_half_kernel<false, 1, 1><<<2 * B, 256, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, htr);
-        else if (bb.dy && addend)
-            tr::conv_wino_half_kernel<true, 2, 2><<<2 * B, 256, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, htr);
-        else if (bb.dy)
-            tr::conv_wino_half_kernel<false, 2, 2><<<2 * B, 256, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, htr);
-        else if (addend && stats == 2)
-            tr::conv_wino_half_kernel<true, 2, 0><<<2 * B, 256, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, htr);
-        else if (addend && stats == 0)
-            tr::conv_wino_half_kernel<true, 0, 0><<<2 * B, 256, 0, T->st>>>(X, U4, ub, bias, addend, Y, bs, bn, bb, B, htr);
-        else if (!addend && stats == 1)
-            tr::conv_wino_half_kernel<false, 1, 0><<<2 * B, 256, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, htr);
-        else if (!addend && stats == 2)
-            tr::conv_wino_half_kernel<false, 2, 0><<<2 * B, 256, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, htr);
-        else if (!addend && stats == 0)
-            tr::conv_wino_half_kernel<false, 0, 0><<<2 * B, 256, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, htr);
-        else
-            return fail("Winograd conv: unsupported statistics mode");
-        return hipGetLastError() == hipSuccess ? 0 : fail("Winograd conv launch failed");
-    }
+    // small batches (the 512 / world shard of a sharded step): two half-channel (2B <= 256) or four
+    // quarter-channel (4B <= 256) workgroups per board fill more CUs (conv_wino_part_kernel,
+    // bit-identical to the one-board kernel)
+    const int np = T->half >= 0 ? T->half : (4 * B <= AZ_TRAIN_WG ? 4 : 2 * B <= AZ_TRAIN_WG ? 2 : 0);
+    if (np == 2) return launch_wino_part<2>(T, X, U4, ub, bias, addend, Y, B, stats, bs, bn, bb);
+    if (np == 4) return launch_wino_part<4>(T, X, U4, ub, bias, addend, Y, B, stats, bs, bn, bb);
+    if (np != 0) return fail("Winograd conv: AZ_TRAIN_HALF must be -1, 0, 2 or 4");
     const unsigned wg = (unsigned)std::min(B, AZ_TRAIN_WG);   // persistent workgroups (one per CU)
     // ORC: O's sign recomputed (no residual: BN 0 and BN1s) where the host asks for it
     const int orc = (bb.dy && bb.beta ? 1 : 0) | (stats == 2 && bs.gamma ? 2 : 0);

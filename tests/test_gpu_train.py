@@ -297,25 +297,27 @@ def test_bn_staging_matches_separate_bn_kernels(require_gpu, monkeypatch, blocks
     assert checked > 4 * blocks
 
 
-@pytest.mark.parametrize("blocks,n,fuse", [(20, 4, "1"), (2, 80, "1"), (2, 80, "0"), (3, 13, "0"), (2, 128, "1")])
-def test_half_workgroup_convs_bit_identical(require_gpu, monkeypatch, blocks, n, fuse):
-    """Round 6: at small batches (2 B <= 256, the 512 / world shard of a sharded step at world >= 4)
-    the Winograd convs run as two half-channel workgroups per board (conv_wino_half_kernel, so
-    twice the CUs work); against the persistent one-board kernel (AZ_TRAIN_HALF=0): the same MFMA
-    accumulation order, transforms, BatchNorm staging and per-board statistics, so two steps give
-    bit-identical losses, gradients and parameters.  n = 80 / 128 map both halves of a board to one
-    XCD (n % 8 == 0), n = 4 / 13 take the plain board order; fuse = "0" runs the convs without
-    BatchNorm staging (AZ_TRAIN_FUSE_BN=0)."""
+@pytest.mark.parametrize("blocks,n,fuse,parts", [(20, 4, "1", "4"), (2, 80, "1", "2"), (2, 80, "0", "4"),
+                                                 (3, 13, "0", "2"), (2, 64, "1", "4"), (2, 128, "1", "2")])
+def test_part_workgroup_convs_bit_identical(require_gpu, monkeypatch, blocks, n, fuse, parts):
+    """Round 6: at small batches (the 512 / world shard of a sharded step) the Winograd convs run as
+    two half-channel or four quarter-channel workgroups per board (conv_wino_part_kernel: the
+    default when 2B or 4B <= 256, so that 2x / 4x the CUs work); against the persistent one-board
+    kernel (AZ_TRAIN_HALF=0): the same MFMA accumulation order per accumulator (the quarters
+    interleave two steps' chains), transforms, BatchNorm staging and per-board statistics, so two
+    steps give bit-identical losses, gradients and parameters.  n = 64 / 80 / 128 map a board's
+    parts to one XCD (n % 8 == 0), n = 4 / 13 take the plain board order; fuse = "0" runs the convs
+    without BatchNorm staging (AZ_TRAIN_FUSE_BN=0)."""
     w = A.random_weights(blocks, 256, seed=17)
     planes, tpol, tval = batch(n, seed=300 + n)
     monkeypatch.setenv("AZ_TRAIN_FUSE_BN", fuse)
     out = {}
-    for flag in ("-1", "0"):
+    for flag in (parts, "0"):
         monkeypatch.setenv("AZ_TRAIN_HALF", flag)
         tr = A.Trainer(blocks, 256, weights=w, max_batch=n)
         losses = [tr.step(planes, tpol, tval, A.get_cyclical_lr(it)) for it in range(2)]
         out[flag] = (losses, tr.grads(), tr.params())
-    (l1, g1, p1), (l0, g0, p0) = out["-1"], out["0"]
+    (l1, g1, p1), (l0, g0, p0) = out[parts], out["0"]
     assert l1 == l0
     assert np.array_equal(g1, g0), np.abs(g1 - g0).max()
     assert np.array_equal(p1, p0), np.abs(p1 - p0).max()
