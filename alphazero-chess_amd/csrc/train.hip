@@ -263,21 +263,17 @@ __device__ __forceinline__ f32x4 wino_comb(int k, f32x4 a, f32x4 b) { return k =
 // 22.57 ms per step (transform mid-board / after the last quad) against 22.35 -- and a
 // branch-free sign-mask form of wino_comb, 23.21: both spill (4-12 VGPRs) at the 256-VGPR cap;
 // profiles/r05h_train_ab.txt.  Not kept.)
-// GLDS (round 6): X comes in by LDS-DMA (`buffer_load_dwordx4 ... lds`, no VGPR destination) into
-// a raw image of the board, and only the squares point xi reads: r = 0 reads the odd rows, r = 3 the
-// even ones, 1 and 2 all of them (the same for q and the columns), so a corner point's workgroup
-// issues 16 loads of X per board, an edge point's 32 and a centre point's 64 -- 576 instead of 1,024
-// per (split, board) over the 16 points -- and the register prefetch of X (32 VGPRs) is gone.  Off-
-// board squares read a zero square.  The transform reads the squares from the image.  dY stays
-// register-staged.
-template <bool GLDS>
+// (Round 6: X by LDS-DMA into a raw board image of only the point's distinct squares -- a corner
+// point's workgroup then issues 16 X loads per board instead of 64, 576 instead of 1,024 per split
+// and board -- bit-identical, measured 22.43 vs 21.93 ms per step at B = 512 and flat at 64,
+// profiles/r06h_ab_glds_b512.txt: the per-board vmcnt(0) drain at the staging barrier and the
+// image's LDS reads cost more than the load instructions saved.  Not kept.)
 __global__ void __launch_bounds__(512)
 wino_wgrad_gemm_kernel(const float* __restrict__ X, const float* __restrict__ DY, int K, int rows_per_split,
                        float* __restrict__ partial) {
     constexpr int NWG = 8, F = 256, CO = F / NWG, NN = CO / 16, TPT = 16 / NWG;
     __shared__ __attribute__((aligned(16))) float xs[16 * WG_SX];
     __shared__ __attribute__((aligned(16))) float ds[16 * WG_SD];
-    __shared__ __attribute__((aligned(16))) float xr[GLDS ? 65 * F : 4];   // [square][channel], square 64 = zeros
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int split = blockIdx.x, xi = blockIdx.y, r = xi >> 2, q = xi & 3;
     const int i1 = r == 0 ? 0 : 1, i2 = r == 3 ? 3 : 2, j1 = q == 0 ? 0 : 1, j2 = q == 3 ? 3 : 2;
@@ -298,36 +294,20 @@ wino_wgrad_gemm_kernel(const float* __restrict__ X, const float* __restrict__ DY
     const __amdgpu_buffer_rsrc_t rD = __builtin_amdgcn_make_buffer_rsrc((void*)DY, (short)0, xbytes, 0x00020000);
     constexpr int OFF_BOARD = 0x40000000;       // past any buffer this kernel is given (< 1 GiB, host-checked)
     f32x4 xd[TPT][2][2], yv[TPT][2][2];   // [tile][patch row i1 / i2][patch column j1 / j2], [tile][a][b]
-    // GLDS: the point's distinct squares (rows / columns of its parity), wave w loads squares w, w + 8, ...
-    const int nr = (r == 0 || r == 3) ? 4 : 8, nc = (q == 0 || q == 3) ? 4 : 8;
-    if constexpr (GLDS) {
-        for (int c = tid; c < F / 4; c += 512) reinterpret_cast<float4*>(xr + 64 * F)[c] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
     auto fetch = [&](int rc) {
         const int bb0 = (rc >> 4) * 64 * F * 4;
-        if constexpr (GLDS) {
-            for (int k = tp; k < nr * nc; k += NWG) {   // wave-uniform: one 1 KB square per instruction
-                const int kr = k / nc, kc = k % nc;
-                const int row = r == 0 ? 2 * kr + 1 : r == 3 ? 2 * kr : kr, col = q == 0 ? 2 * kc + 1 : q == 3 ? 2 * kc : kc;
-                const int sq = __builtin_amdgcn_readfirstlane(row * 8 + col);
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (__attribute__((address_space(3))) void*)(xr + sq * F), 16, c4 * 4,
-                                                         bb0 + sq * F * 4, 0, 0);
-            }
-        }
 #pragma unroll
         for (int u = 0; u < TPT; u++) {
             const int t = TPT * tp + u, ty = t >> 2, tx = t & 3;
-            if constexpr (!GLDS) {
 #pragma unroll
-                for (int ii = 0; ii < 2; ii++)
+            for (int ii = 0; ii < 2; ii++)
 #pragma unroll
-                    for (int jj = 0; jj < 2; jj++) {
-                        const int row = 2 * ty - 1 + (ii ? i2 : i1), col = 2 * tx - 1 + (jj ? j2 : j1);
-                        const bool on = (unsigned)row < 8u && (unsigned)col < 8u;
-                        xd[u][ii][jj] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                                      rX, on ? c4 * 4 : OFF_BOARD, on ? bb0 + (row * 8 + col) * F * 4 : 0, 0));
-                    }
-            }
+                for (int jj = 0; jj < 2; jj++) {
+                    const int row = 2 * ty - 1 + (ii ? i2 : i1), col = 2 * tx - 1 + (jj ? j2 : j1);
+                    const bool on = (unsigned)row < 8u && (unsigned)col < 8u;
+                    xd[u][ii][jj] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                  rX, on ? c4 * 4 : OFF_BOARD, on ? bb0 + (row * 8 + col) * F * 4 : 0, 0));
+                }
 #pragma unroll
             for (int a = 0; a < 2; a++)
 #pragma unroll
@@ -338,22 +318,10 @@ wino_wgrad_gemm_kernel(const float* __restrict__ X, const float* __restrict__ DY
     };
     if (rbeg < rend) fetch(rbeg);
     for (int rc = rbeg; rc < rend; rc += 16) {
-        if constexpr (GLDS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA landed
-        __syncthreads();                                                     // ... and every wave's
+        __syncthreads();
 #pragma unroll
         for (int u = 0; u < TPT; u++) {
             const int t = TPT * tp + u;
-            if constexpr (GLDS) {   // the tile's four squares from the raw image (off-board: the zero square)
-                const int ty = t >> 2, tx = t & 3;
-#pragma unroll
-                for (int ii = 0; ii < 2; ii++)
-#pragma unroll
-                    for (int jj = 0; jj < 2; jj++) {
-                        const int row = 2 * ty - 1 + (ii ? i2 : i1), col = 2 * tx - 1 + (jj ? j2 : j1);
-                        const bool on = (unsigned)row < 8u && (unsigned)col < 8u;
-                        xd[u][ii][jj] = *reinterpret_cast<const f32x4*>(xr + (on ? row * 8 + col : 64) * F + c4);
-                    }
-            }
             // V: rows first (tt over the two columns), then the column combination
             const f32x4 tt1 = wino_comb(r, xd[u][0][0], xd[u][1][0]), tt2 = wino_comb(r, xd[u][0][1], xd[u][1][1]);
             const f32x4 v = wino_comb(q, tt1, tt2);
@@ -1786,7 +1754,6 @@ struct Trainer {
     int xev_used = 0;
     bool fuse_bn = true;                     // BN apply / backward staged in the next Winograd conv (env AZ_TRAIN_FUSE_BN=0: off)
     bool orc = true;                         // O's sign recomputed where no residual (env AZ_TRAIN_ORC=0: off)
-    bool wgrad_glds = true;                  // Winograd weight grad: X by LDS-DMA (env AZ_TRAIN_WGRAD_GLDS=0: registers)
     int half = -1;                           // conv workgroups per board at small batches: -1 auto (4 when 4B <= the CU
                                              // count, 2 when 2B <=), 0 one per board, 2 / 4 always (env AZ_TRAIN_HALF)
     // the conv bias gradients of the tower's BatchNorms: bn_back4 partials per BN, summed in one
@@ -1883,10 +1850,12 @@ int launch_wino(Trainer* T, const float* X, const float* U, const float* bias, c
         trb = g_trace + (size_t)(g_trace_n++ % TRACE_LAUNCHES) * TRACE_BOARDS * 8;
     }
 #endif
-    // small batches (the 512 / world shard of a sharded step): two half-channel (2B <= 256) or four
-    // quarter-channel (4B <= 256) workgroups per board fill more CUs (conv_wino_part_kernel,
-    // bit-identical to the one-board kernel)
-    const int np = T->half >= 0 ? T->half : (4 * B <= AZ_TRAIN_WG ? 4 : 2 * B <= AZ_TRAIN_WG ? 2 : 0);
+    // small batches (the 512 / world shard of a sharded step): four quarter-channel workgroups per
+    // board when 2B <= 256 fill the CUs the one-board kernel leaves idle (conv_wino_part_kernel,
+    // bit-identical to it).  Step at B = 64: 6.78 ms against 7.90 (halves) and 8.93 (one board);
+    // B = 128: 8.24 / 8.93 / 9.87 (profiles/r06g_ab_parts_b*.txt); at B = 256 halves lose (12.37 vs
+    // 11.96, r06e)
+    const int np = T->half >= 0 ? T->half : (2 * B <= AZ_TRAIN_WG ? 4 : 0);
     if (np == 2) return launch_wino_part<2>(T, X, U4, ub, bias, addend, Y, B, stats, bs, bn, bb);
     if (np == 4) return launch_wino_part<4>(T, X, U4, ub, bias, addend, Y, B, stats, bs, bn, bb);
     if (np != 0) return fail("Winograd conv: AZ_TRAIN_HALF must be -1, 0, 2 or 4");
@@ -1970,10 +1939,7 @@ int launch_wino_wgrad(Trainer* T, const float* X, const float* DY, int B, float*
     if ((size_t)B * 64 * F * 4 >= (size_t)0x40000000) return fail("Winograd wgrad: batch too large for 32-bit offsets");
     if ((size_t)F * F % 256) return fail("Winograd wgrad: F * F must be a multiple of 256");
     const unsigned rblocks = (unsigned)((size_t)F * F / 256);
-    if (T->wgrad_glds)
-        tr::wino_wgrad_gemm_kernel<true><<<dim3(splits, 16), 512, 0, T->st>>>(X, DY, K, wino_gemm_rows(B), T->wpart);
-    else
-        tr::wino_wgrad_gemm_kernel<false><<<dim3(splits, 16), 512, 0, T->st>>>(X, DY, K, wino_gemm_rows(B), T->wpart);
+    tr::wino_wgrad_gemm_kernel<<<dim3(splits, 16), 512, 0, T->st>>>(X, DY, K, wino_gemm_rows(B), T->wpart);
     tr::wino_wgrad_reduce_out_kernel<<<rblocks, 1024, 0, T->st>>>(T->wpart, splits, F, g);
     return hipGetLastError() == hipSuccess ? 0 : fail("Winograd wgrad launch failed");
 }
@@ -2700,7 +2666,6 @@ int az_trainer_create(int blocks, int filters, const float* weights, size_t n, i
     if (const char* e = getenv("AZ_TRAIN_FUSE_BN")) T->fuse_bn = atoi(e) != 0;
     if (const char* e = getenv("AZ_TRAIN_ORC")) T->orc = atoi(e) != 0;
     if (const char* e = getenv("AZ_TRAIN_HALF")) T->half = atoi(e);
-    if (const char* e = getenv("AZ_TRAIN_WGRAD_GLDS")) T->wgrad_glds = atoi(e) != 0;
     if (!ok) { delete T; return fail("az_trainer_create: out of device memory"); }
     // parameters, zero moments, trainable mask (BatchNorm running statistics are not parameters)
     std::vector<uint8_t> mask(T->np, 1);

@@ -236,18 +236,15 @@ def test_winograd_training_convs_match_direct(require_gpu, monkeypatch):
         assert np.linalg.norm(g1[o:o + cnt] - r) <= 1e-2 * max(np.linalg.norm(r), 1e-30), name
 
 
-@pytest.mark.parametrize("knob,fuse,n", [("AZ_TRAIN_ORC", "1", 300), ("AZ_TRAIN_ORC", "0", 37),
-                                         ("AZ_TRAIN_WGRAD_GLDS", "1", 300), ("AZ_TRAIN_WGRAD_GLDS", "1", 5)])
+@pytest.mark.parametrize("knob,fuse,n", [("AZ_TRAIN_ORC", "1", 300), ("AZ_TRAIN_ORC", "0", 37)])
 def test_round6_conv_changes_are_bit_identical(require_gpu, monkeypatch, knob, fuse, n):
-    """Round 6, each change against its A/B knob.  AZ_TRAIN_ORC: for a BatchNorm with no residual
+    """Round 6, AZ_TRAIN_ORC: for a BatchNorm with no residual
     (BN 0, every block's BN1) the data-grad conv recomputes O > 0 as ((Y - mean) / std) * gamma +
     beta > 0 (the forward's own float expression) instead of reading O, in the BN-backward staging
     and in the STATS 2 epilogue (fused and unfused BN paths; n = 300: the persistent one-board
     kernel, 44 workgroups take two boards; n = 37: the half-channel kernel, which reads O either
-    way).  AZ_TRAIN_WGRAD_GLDS: the weight grad's X squares by LDS-DMA into a raw board image, only
-    the point's distinct squares (n = 300: 16 splits of 19 boards, the last of 15; n = 5: one board per split).
-    Losses, running statistics and every gradient bit-identical over two steps (the second from the
-    AdamW-updated weights)."""
+    way).  Losses, running statistics and every gradient bit-identical over two steps (the second
+    from the AdamW-updated weights)."""
     blocks = 3
     w = A.random_weights(blocks, 256, seed=29)
     planes, tpol, tval = batch(n, seed=501)
