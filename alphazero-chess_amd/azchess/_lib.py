@@ -140,6 +140,7 @@ SIGNATURES = [
     ("az_replay_destroy", C.c_int, [C.c_void_p]),
     ("az_replay_len", C.c_int, [C.c_void_p]),
     ("az_replay_add", C.c_int, [C.c_void_p, P(AzEpisodeStep)]),
+    ("az_replay_add_many", C.c_int, [C.c_void_p, P(AzEpisodeStep), C.c_int]),
     ("az_replay_add_dense", C.c_int, [C.c_void_p, P(AzPos), P(C.c_float), C.c_float]),
     ("az_replay_sample", C.c_int, [C.c_void_p, C.c_int, C.c_uint64, P(C.c_float), P(C.c_float), P(C.c_float),
                                    P(AzPos)]),

@@ -55,7 +55,10 @@ class ReplayBuffer:
                                                  float(step.final_value)))
 
     def add_many(self, steps):
-        """add() every step in order; returns the number of new unique positions."""
+        """add() every step in order; returns the number of new unique positions.  A ctypes array
+        of az_episode_step (unpack_steps, a drain) goes to the engine in one call."""
+        if isinstance(steps, C.Array) and issubclass(steps._type_, L.AzEpisodeStep):
+            return L.check(L.lib.az_replay_add_many(self._h, steps, len(steps))) if len(steps) else 0
         return sum(self.add(s) for s in steps)
 
     def sample_arrays(self, batch_size, seed):

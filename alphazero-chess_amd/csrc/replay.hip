@@ -150,6 +150,17 @@ int az_replay_add(az_replay* r, const az_episode_step* st) {
     return replay_add(r, fen_of(&st->state), pol.data(), st->final_value);
 }
 
+int az_replay_add_many(az_replay* r, const az_episode_step* steps, int n) {
+    if (!r || n < 0 || (n > 0 && !steps)) return fail("az_replay_add_many: bad arguments");
+    int added = 0;
+    for (int i = 0; i < n; i++) {   // in order, exactly as n calls of az_replay_add
+        const int rc = az_replay_add(r, steps + i);
+        if (rc < 0) return rc;
+        added += rc;
+    }
+    return added;
+}
+
 int az_replay_add_dense(az_replay* r, const az_pos* state, const float* policy, float value) {
     if (!r || !state || !policy) return fail("null");
     return replay_add(r, fen_of(state), policy, value);

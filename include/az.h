@@ -311,6 +311,9 @@ int az_replay_len(const az_replay* r);                              /* memory.rs
 /* ReplayBuffer::add (memory.rs:41-79): running mean into an existing FEN entry (returns 0) or
  * a new entry at the FIFO's end, evicting the oldest at capacity (returns 1) */
 int az_replay_add(az_replay* r, const az_episode_step* step);
+/* az_replay_add of steps[0..n) in order; returns the number of new unique positions (the union of
+ * every rank's drained steps, added in rank order, keeps the replicas of one buffer identical) */
+int az_replay_add_many(az_replay* r, const az_episode_step* steps, int n);
 int az_replay_add_dense(az_replay* r, const az_pos* state, const float* policy, float value);
 /* ReplayBuffer::sample (memory.rs:81-101): min(batch, len) distinct entries, uniformly (seeded);
  * writes to_tensor planes [n,19,64], policies [n,4096], values [n], positions (any may be NULL).
