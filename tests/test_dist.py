@@ -193,3 +193,18 @@ def test_pack_unpack_steps_round_trip():
         assert False, "truncated payload accepted"
     except ValueError:
         pass
+
+
+def test_train_world2_argument_checks_before_any_device_call():
+    """train() at world > 1 (the reference's train(): one shared buffer, sharded batch) refuses on
+    the host, before a trainer touches a GPU: a global batch smaller than the world, and a shared
+    buffer with no way to exchange EpisodeSteps (no allgather and no torch.distributed group)."""
+    import pytest
+    import azchess as A
+    red = (lambda buf: None, 0, 2)
+    with pytest.raises(ValueError, match="smaller than world"):
+        A.train(1, reducer=red, batch_size=1, allgather=lambda b: [b, b])
+    with pytest.raises(ValueError, match="allgather"):
+        A.train(1, reducer=red)
+    with pytest.raises(ValueError, match="not both"):
+        A.train(1, reducer=red, comm=(b"", 0, 2))
