@@ -33,7 +33,7 @@ PEAK_F32_TFLOPS = 157.3       # MI355X_MICROARCH.md: f32 MFMA = vector peak
 PEAK_HBM_GBS = 8000.0         # MI355X_MICROARCH.md: 8.0 TB/s spec
 # HBM bytes per tower launch from rocprofv3 PMC passes (tools/pmc_run.sh: FETCH_SIZE x2 per the
 # gfx950 correction + WRITE_SIZE), same kernel and per-launch work (2048 rows, 20x256)
-PMC_SUMMARY = {"f32": os.path.join(ROOT, "profiles", "r04_pmc_tower32w_summary.json"),             # Winograd
+PMC_SUMMARY = {"f32": os.path.join(ROOT, "profiles", "r06_pmc_tower32w_summary.json"),             # Winograd
                "f32-direct": os.path.join(ROOT, "profiles", "r02_pmc_tower32_summary.json"),      # AZ_WINOGRAD=0
                "bf16": os.path.join(ROOT, "profiles", "r04_pmc_tower_bf16_summary.json")}
 # simulation steps of the instrumented profile pass after the timed window (8 sampled tower launches)
