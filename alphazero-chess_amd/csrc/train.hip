@@ -559,13 +559,18 @@ __global__ void finalize_var_kernel(const float* __restrict__ part, int nblk, in
 }
 
 // BN backward sums: dbeta[c] = sum dz, dgamma[c] = sum dz*yhat
+// slot (sharded batch): also this rank's exchange slot [dbeta | dgamma] (two copies fewer per BN)
 __global__ void finalize_bnback_kernel(const float* __restrict__ part, int nblk, int C, float* __restrict__ dgamma,
-                                       float* __restrict__ dbeta) {
+                                       float* __restrict__ dbeta, float* __restrict__ slot = nullptr) {
     FIN_CHANNEL();
     const float b = part_sum(part, nblk, C, c, 0, lane), g = part_sum(part, nblk, C, c, 1, lane);
     if (lane == 0) {
         dbeta[c] = b;
         dgamma[c] = g;
+        if (slot) {
+            slot[c] = b;
+            slot[C + c] = g;
+        }
     }
 }
 // BN forward statistics from per-board partials (BoardStats, STATS 1): mean = sum / R, and the
@@ -2157,9 +2162,10 @@ int bn_back_sums(Trainer* T, int bi, const float* dout, const float* O, const fl
     const float* sd = T->bstd + (size_t)bi * T->slot;
     float* dgam = T->g + bn_off;
     float* dbet = T->g + bn_off + C;
+    float* my = T->sharded && xchg ? T->xback + (size_t)T->rank * T->xbs : nullptr;
     if (bpart) {
         if (R % 64 || ld != C) return fail("bn: board statistics need whole boards");
-        tr::finalize_bnback_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(bpart, R / 64, C, dgam, dbet);
+        tr::finalize_bnback_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(bpart, R / 64, C, dgam, dbet, my);
     } else {
         const int nb = nblk_rows(R);
         dim3 g(nb, (C + 63) / 64);
@@ -2169,10 +2175,11 @@ int bn_back_sums(Trainer* T, int bi, const float* dout, const float* O, const fl
     // the gradient keeps this rank's dgamma / dbeta (summed over ranks with the rest of it);
     // sharded, the BN backward itself needs the global sums: exchanged through xback
     const float *ug = dgam, *ub = dbet;
-    if (T->sharded && xchg) {
-        float* my = T->xback + (size_t)T->rank * T->xbs;
-        AZ_HIP(hipMemcpyAsync(my, dbet, C * sizeof(float), hipMemcpyDeviceToDevice, T->st));
-        AZ_HIP(hipMemcpyAsync(my + C, dgam, C * sizeof(float), hipMemcpyDeviceToDevice, T->st));
+    if (my) {
+        if (!bpart) {   // the column-sum path finalized into the gradient only
+            AZ_HIP(hipMemcpyAsync(my, dbet, C * sizeof(float), hipMemcpyDeviceToDevice, T->st));
+            AZ_HIP(hipMemcpyAsync(my + C, dgam, C * sizeof(float), hipMemcpyDeviceToDevice, T->st));
+        }
         TRY(sum_over_ranks(T, 2 * C, "BatchNorm backward sums"));
         ub = T->xsum;
         ug = T->xsum + C;
