@@ -574,6 +574,70 @@ def _allgather_pair():
     return allgather
 
 
+def _host_reducer_n(world):
+    """In-process host reducer for `world` ranks as threads: the element-wise sum in rank order."""
+    import threading
+    slots, bar = [None] * world, threading.Barrier(world, timeout=60)
+
+    def reducer(rank):
+        def reduce(buf):
+            slots[rank] = buf.copy()
+            bar.wait()
+            acc = slots[0].copy()
+            for r in range(1, world):
+                acc += slots[r]
+            buf[:] = acc
+            bar.wait()
+        return reduce
+    return reducer
+
+
+def test_sharded_world4_host_reducer_matches_single_batch(require_gpu):
+    """The sharded step at world 4 (round 6: gathers, rank-order sums): four ranks as threads on one
+    GPU with unequal shards 100 + 156 + 128 + 128 of one 512 batch (the 100 / 128 shards take the
+    quarter-channel convs, 156 the one-board kernel), against one rank on all 512: losses <= 1e-5,
+    every gradient tensor summed over the ranks <= 1e-2 relative norm (ReLU branches near 0),
+    running statistics <= 1e-5 and bit-identical on the four ranks, and the AdamW step leaves the
+    four ranks bit-identical."""
+    blocks, filters, n = 2, 256, 512
+    cuts = [0, 100, 256, 384, 512]
+    w = A.random_weights(blocks, filters, seed=43)
+    planes, tpol, tval = batch(n, seed=44)
+    one = A.Trainer(blocks, filters, weights=w, max_batch=n)
+    l1 = one.compute_gradients(planes, tpol, tval)
+    g1, p1 = one.grads().astype(np.float64), one.params()
+    red = _host_reducer_n(4)
+    ranks = [A.Trainer(blocks, filters, weights=w, max_batch=cuts[r + 1] - cuts[r]) for r in range(4)]
+    for r, tr in enumerate(ranks):
+        tr.set_host_reducer(red(r), r, 4)
+        tr.set_sharded(True)
+    sl = [slice(cuts[r], cuts[r + 1]) for r in range(4)]
+    ls = _run_ranks([lambda r=r, tr=tr: tr.compute_gradients(planes[sl[r]], tpol[sl[r]], tval[sl[r]])
+                     for r, tr in enumerate(ranks)])
+    assert all(l == ls[0] for l in ls)
+    assert abs(ls[0][0] - l1[0]) <= 1e-5 * (1 + abs(l1[0])) and abs(ls[0][1] - l1[1]) <= 1e-5 * (1 + abs(l1[1]))
+    gs = [tr.grads().astype(np.float64) for tr in ranks]
+    gsum = gs[0] + gs[1] + gs[2] + gs[3]
+    ps = [tr.params() for tr in ranks]
+    stats = ~T.trainable_mask(blocks, filters)
+    for p in ps[1:]:
+        assert np.array_equal(p[stats], ps[0][stats])
+    assert np.all(np.abs(ps[0][stats] - p1[stats]) <= 1e-5 * (1 + np.abs(p1[stats])))
+    seg, _ = T.segments(blocks, filters)
+    zero_bias = bn_fed_biases(blocks)
+    for name, (o, shape, bn) in seg.items():
+        if name in zero_bias:
+            continue
+        cnt = 2 * shape[1] if bn else int(np.prod(shape))
+        r = g1[o:o + cnt]
+        assert np.linalg.norm(gsum[o:o + cnt] - r) <= 1e-2 * max(np.linalg.norm(r), 1e-30), name
+    lr = A.get_cyclical_lr(3)
+    _run_ranks([lambda tr=tr: tr.apply(lr) for tr in ranks])
+    after = [tr.params() for tr in ranks]
+    for p in after[1:]:
+        assert np.array_equal(p, after[0])
+
+
 def test_train_loop_one_global_buffer_two_ranks(require_gpu, tmp_path):
     """train() at world 2 computes the reference's train() (training.rs:81-159,
     memory.rs:41-96) -- two ranks as threads on one GPU, gradient / BatchNorm exchanges through a host
