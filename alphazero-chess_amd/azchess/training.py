@@ -70,16 +70,26 @@ class SelfPlay:
     def drain(self):
         return [_convert(s) for s in self.drain_raw()]
 
+    _drain_buf = None
+
     def drain_raw(self):
         """EpisodeSteps of the games that ended, as the engine's az_episode_step records (what
-        ReplayBuffer.add takes directly)."""
-        out = []
+        ReplayBuffer.add takes directly): a right-sized array per call (the 4 MB staging buffer is
+        reused, so a pass that keeps its drains holds only the steps themselves)."""
+        if self._drain_buf is None:
+            self._drain_buf = (L.AzEpisodeStep * 4096)()
+        buf, parts = self._drain_buf, []
         while True:
-            buf = (L.AzEpisodeStep * 4096)()
             n = L.check(L.lib.az_selfplay_drain(self.search._h, buf, 4096))
-            out += [buf[i] for i in range(n)]
+            if n:
+                arr = (L.AzEpisodeStep * n)()
+                C.memmove(arr, buf, n * C.sizeof(L.AzEpisodeStep))
+                parts.append(arr)
             if n < 4096:
-                return out
+                break
+        if len(parts) == 1:
+            return parts[0]
+        return (L.AzEpisodeStep * sum(len(p) for p in parts))(*[s for p in parts for s in p])
 
 
 def run_all_episodes(model=None, games=100, max_moves=1000, device=0, **cfg):
@@ -347,13 +357,19 @@ def train(iterations, blocks=NUM_RES_BLOCKS, filters=NUM_FILTERS, games=NUM_EPIS
                 drained = sp.drain_raw()
                 steps_done += len(drained)
                 if shared_replay and world > 1:
-                    local += drained
+                    local.append(drained)
                 else:
                     new_unique += replay.add_many(drained)
                 if active == 0:
                     break
             if shared_replay and world > 1:
-                nu, added = add_from_ranks(replay, local, allgather)
+                nsteps = sum(len(d) for d in local)
+                allsteps = (L.AzEpisodeStep * nsteps)()
+                o = 0
+                for d in local:   # this pass's drains in order, one contiguous array
+                    C.memmove(C.byref(allsteps, o * C.sizeof(L.AzEpisodeStep)), d, len(d) * C.sizeof(L.AzEpisodeStep))
+                    o += len(d)
+                nu, added = add_from_ranks(replay, allsteps, allgather)
                 new_unique += nu
                 steps_global += added
             plays += 1
