@@ -29,6 +29,7 @@
 #include <algorithm>
 #include <initializer_list>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "az_internal.h"
@@ -388,6 +389,166 @@ wino_wgrad_gemm_kernel(const float* __restrict__ X, const float* __restrict__ DY
                     const int ci = 64 * j + 4 * (4 * (lane >> 4) + g) + c, co = CO * w + 16 * n + (lane & 15);
                     out[(size_t)ci * F + co] = acc[4 * j + c][n][g];
                 }
+}
+
+// f(std::integral_constant<int, I>) for I = 0 .. N-1, unrolled by construction (a #pragma unroll over
+// the weight grad's 256-MFMA board with its side jobs was left rolled, and its indexed register
+// arrays went to scratch)
+template <class Fn, int... Is>
+__device__ __forceinline__ void static_for_impl(Fn&& f, std::integer_sequence<int, Is...>) {
+    (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, class Fn>
+__device__ __forceinline__ void static_for(Fn&& f) { static_for_impl(f, std::make_integer_sequence<int, N>{}); }
+// The same weight grad with one wave per SIMD (round 6, the default): 4 waves, wave w owns co
+// [64 w, 64 w + 64) x all 256 ci -- 256 accumulators per lane, in AGPRs, updated in place by inline
+// asm MFMAs (with the builtin, 256 live accumulators made the allocator copy them between AGPRs
+// and VGPRs every board) -- and the transformed board in two LDS buffers.  While board b's MFMAs
+// run from one buffer, the wave transforms board b + 1's squares (loaded a board earlier) into the
+// other and issues board b + 2's loads into the registers just freed, in small steps between single
+// MFMAs, so that per board only one barrier and the first quad's LDS reads are exposed.  The point
+// (r, q) is a template parameter (one body per point, chosen by blockIdx.y), so a transform step is
+// four adds.  Every accumulator gets the same MFMA sequence as in wino_wgrad_gemm_kernel (rows in
+// order, four per MFMA) and the transforms the same operations: the partials are bit-identical
+// (test_weight_grad_one_wave_per_simd_bit_identical).  Measured at B = 512
+// (profiles/r06s_*): 148.6 us against 164-168 us, and 130.9 us with the side jobs removed (a
+// pricing build, wrong results): the transforms and loads cost the one MFMA wave ~12 %, which
+// fillers of 16-24 cycles per 32-cycle f32 MFMA gap do not hide.
+template <int R, int Q>
+__device__ __forceinline__ void wgrad4_body(const float* __restrict__ X, const float* __restrict__ DY, int K,
+                                            int rows_per_split, float* __restrict__ partial, float* xsm, float* dsm) {
+    constexpr int NWV = 4, F = 256, CO = F / NWV, NN = CO / 16, TPT = 16 / NWV;
+    constexpr int XB = 16 * WG_SX, DB = 16 * WG_SD;   // one LDS buffer of V / M' rows
+    constexpr int I1 = R == 0 ? 0 : 1, I2 = R == 3 ? 3 : 2, J1 = Q == 0 ? 0 : 1, J2 = Q == 3 ? 3 : 2;
+    constexpr float RA = R == 3 ? 0.0f : 1.0f, RB = R == 0 ? 0.0f : (R == 1 ? 1.0f : -1.0f);
+    constexpr float QA = Q == 3 ? 0.0f : 1.0f, QB = Q == 0 ? 0.0f : (Q == 1 ? 1.0f : -1.0f);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int split = blockIdx.x;
+    const int rbeg = split * rows_per_split, rend = min(K, rbeg + rows_per_split), nbd = (rend - rbeg) >> 4;
+    f32x4 acc[16][NN];
+#pragma unroll
+    for (int b = 0; b < 16; b++)
+#pragma unroll
+        for (int n = 0; n < NN; n++) acc[b][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int c4 = lane * 4, tp = __builtin_amdgcn_readfirstlane(w);
+    const int xbytes = (K >> 4) * 64 * F * 4;
+    const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, xbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rD = __builtin_amdgcn_make_buffer_rsrc((void*)DY, (short)0, xbytes, 0x00020000);
+    constexpr int OFF_BOARD = 0x40000000;
+    f32x4 xd[TPT][2][2], yv[TPT][2][2];
+    // wino_comb and the M' combination of wino_wgrad_gemm_kernel with the point's constants, in six
+    // steps of four floats (so that one step fits beside one MFMA)
+    f32x4 t1[TPT], t2[TPT], p0[TPT], p1[TPT];
+    auto xstep = [&](int buf, int u, int st) {
+        const int t = TPT * tp + u;
+        if (st == 0) t1[u] = wino_comb(R, xd[u][0][0], xd[u][1][0]);
+        if (st == 1) t2[u] = wino_comb(R, xd[u][0][1], xd[u][1][1]);
+        if (st == 2) *reinterpret_cast<f32x4*>(xsm + buf * XB + t * WG_SX + c4) = wino_comb(Q, t1[u], t2[u]);
+        if (st == 3) p0[u] = yv[u][0][0] * RA + yv[u][1][0] * RB;
+        if (st == 4) p1[u] = yv[u][0][1] * RA + yv[u][1][1] * RB;
+        if (st == 5) *reinterpret_cast<f32x4*>(dsm + buf * DB + t * WG_SD + c4) = p0[u] * QA + p1[u] * QB;
+    };
+    auto xform_tile = [&](int buf, int u) {
+#pragma unroll
+        for (int st = 0; st < 6; st++) xstep(buf, u, st);
+    };
+    // load i of tile u of board bi: X squares i = 0-3, dY squares 4-7 (bi >= nbd: zeros, no branch)
+    auto load1 = [&](int bi, int u, int i) {
+        const bool inb = bi < nbd;
+        const int bb0 = inb ? ((rbeg >> 4) + bi) * 64 * F * 4 : 0, vin = inb ? c4 * 4 : OFF_BOARD;
+        const int t = TPT * tp + u, ty = t >> 2, tx = t & 3;
+        if (i < 4) {
+            const int ii = i >> 1, jj = i & 1;
+            const int row = 2 * ty - 1 + (ii ? I2 : I1), col = 2 * tx - 1 + (jj ? J2 : J1);
+            const bool on = (unsigned)row < 8u && (unsigned)col < 8u;
+            xd[u][ii][jj] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                          rX, on ? vin : OFF_BOARD, on ? bb0 + (row * 8 + col) * F * 4 : 0, 0));
+        } else {
+            const int a = (i - 4) >> 1, bb = i & 1;
+            yv[u][a][bb] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                         rD, vin, bb0 + ((2 * ty + a) * 8 + 2 * tx + bb) * F * 4, 0));
+        }
+    };
+    if (nbd > 0) {
+#pragma unroll
+        for (int u = 0; u < TPT; u++)
+#pragma unroll
+            for (int i = 0; i < 8; i++) load1(0, u, i);
+#pragma unroll
+        for (int u = 0; u < TPT; u++) xform_tile(0, u);
+#pragma unroll
+        for (int u = 0; u < TPT; u++)
+#pragma unroll
+            for (int i = 0; i < 8; i++) load1(1, u, i);
+    }
+    __syncthreads();
+    float bv[2][NN];
+    f32x4 av[2][4];
+    for (int b = 0; b < nbd; b++) {
+        const int cur = b & 1, nxt = cur ^ 1;
+        auto rd = [&](int qq) {
+            const int rq = qq * 4 + (lane >> 4), o = qq & 1;
+#pragma unroll
+            for (int n = 0; n < NN; n++) bv[o][n] = dsm[cur * DB + rq * WG_SD + CO * w + 16 * n + (lane & 15)];
+#pragma unroll
+            for (int j = 0; j < 4; j++) av[o][j] = *reinterpret_cast<const f32x4*>(xsm + cur * XB + rq * WG_SX + 64 * j + 4 * (lane & 15));
+        };
+        // side jobs beside the MFMAs of row quad u (k = its MFMA index, 0..63): the six transform
+        // steps of board b + 1's tile u at k = 0, 2, .., 10, then board b + 2's eight loads of
+        // that tile into the registers just freed, six MFMAs apart from k = 16 (a load costs the
+        // issuing wave more than one MFMA gap, so they are spread over the board)
+        auto side = [&](auto U, auto KK) {
+            constexpr int u = decltype(U)::value, k = decltype(KK)::value;
+            if constexpr (k <= 10 && k % 2 == 0) xstep(nxt, u, k / 2);
+            if constexpr (k >= 16 && (k - 16) % 6 == 0 && (k - 16) / 6 < 8) load1(b + 2, u, (k - 16) / 6);
+        };
+        rd(0);
+        static_for<16>([&](auto G) {
+            constexpr int g = decltype(G)::value, qq = g >> 2, j = g & 3, o = qq & 1;
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (g == 0) rd(1);
+            if constexpr (g == 4) rd(2);
+            if constexpr (g == 8) rd(3);
+            __builtin_amdgcn_sched_barrier(0);
+            static_for<4 * NN>([&](auto CN) {
+                constexpr int c = decltype(CN)::value / NN, n = decltype(CN)::value % NN, k = 16 * j + 4 * c + n;
+                asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+a"(acc[4 * j + c][n]) : "v"(av[o][j][c]), "v"(bv[o][n]));
+                if constexpr ((k <= 10 && k % 2 == 0) || (k >= 16 && (k - 16) % 6 == 0 && (k - 16) / 6 < 8)) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    side(std::integral_constant<int, qq>{}, std::integral_constant<int, k>{});
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            });
+        });
+        __builtin_amdgcn_sched_barrier(0);
+        __syncthreads();
+    }
+    // the MFMAs are inline asm: the compiler does not count their latency before the AGPR reads
+    asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+    float* out = partial + ((size_t)split * 16 + 4 * R + Q) * F * F;
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+#pragma unroll
+            for (int n = 0; n < NN; n++)
+#pragma unroll
+                for (int g = 0; g < 4; g++) {
+                    const int ci = 64 * j + 4 * (4 * (lane >> 4) + g) + c, co = CO * w + 16 * n + (lane & 15);
+                    out[(size_t)ci * F + co] = acc[4 * j + c][n][g];
+                }
+}
+__global__ void __launch_bounds__(256)
+wino_wgrad_gemm4_kernel(const float* __restrict__ X, const float* __restrict__ DY, int K, int rows_per_split,
+                        float* __restrict__ partial) {
+    __shared__ __attribute__((aligned(16))) float xs[2 * 16 * WG_SX];
+    __shared__ __attribute__((aligned(16))) float ds[2 * 16 * WG_SD];
+#define AZ_WG4(x) case x: wgrad4_body<((x) / 4), ((x) % 4)>(X, DY, K, rows_per_split, partial, xs, ds); break;
+    switch (blockIdx.y) {
+        AZ_WG4(0) AZ_WG4(1) AZ_WG4(2) AZ_WG4(3) AZ_WG4(4) AZ_WG4(5) AZ_WG4(6) AZ_WG4(7)
+        AZ_WG4(8) AZ_WG4(9) AZ_WG4(10) AZ_WG4(11) AZ_WG4(12) AZ_WG4(13) AZ_WG4(14) AZ_WG4(15)
+    }
+#undef AZ_WG4
 }
 
 // out[e] = sum over splits s (in order) of partial[s][e]
@@ -1761,6 +1922,7 @@ struct Trainer {
     bool orc = true;                         // O's sign recomputed where no residual (env AZ_TRAIN_ORC=0: off)
     int half = -1;                           // conv workgroups per board at small batches: -1 auto (4 when 4B <= the CU
                                              // count, 2 when 2B <=), 0 one per board, 2 / 4 always (env AZ_TRAIN_HALF)
+    bool wgrad4 = true;                      // weight grad with one wave per SIMD (env AZ_TRAIN_WGRAD4=0: the 8-wave kernel)
     // the conv bias gradients of the tower's BatchNorms: bn_back4 partials per BN, summed in one
     // launch at the end of the backward (bias_dst[j] = gradient offset of BN j's conv bias)
     float* bsum_all = nullptr;
@@ -1944,7 +2106,8 @@ int launch_wino_wgrad(Trainer* T, const float* X, const float* DY, int B, float*
     if ((size_t)B * 64 * F * 4 >= (size_t)0x40000000) return fail("Winograd wgrad: batch too large for 32-bit offsets");
     if ((size_t)F * F % 256) return fail("Winograd wgrad: F * F must be a multiple of 256");
     const unsigned rblocks = (unsigned)((size_t)F * F / 256);
-    tr::wino_wgrad_gemm_kernel<<<dim3(splits, 16), 512, 0, T->st>>>(X, DY, K, wino_gemm_rows(B), T->wpart);
+    if (T->wgrad4) tr::wino_wgrad_gemm4_kernel<<<dim3(splits, 16), 256, 0, T->st>>>(X, DY, K, wino_gemm_rows(B), T->wpart);
+    else tr::wino_wgrad_gemm_kernel<<<dim3(splits, 16), 512, 0, T->st>>>(X, DY, K, wino_gemm_rows(B), T->wpart);
     tr::wino_wgrad_reduce_out_kernel<<<rblocks, 1024, 0, T->st>>>(T->wpart, splits, F, g);
     return hipGetLastError() == hipSuccess ? 0 : fail("Winograd wgrad launch failed");
 }
@@ -2673,6 +2836,7 @@ int az_trainer_create(int blocks, int filters, const float* weights, size_t n, i
     if (const char* e = getenv("AZ_TRAIN_FUSE_BN")) T->fuse_bn = atoi(e) != 0;
     if (const char* e = getenv("AZ_TRAIN_ORC")) T->orc = atoi(e) != 0;
     if (const char* e = getenv("AZ_TRAIN_HALF")) T->half = atoi(e);
+    if (const char* e = getenv("AZ_TRAIN_WGRAD4")) T->wgrad4 = atoi(e) != 0;
     if (!ok) { delete T; return fail("az_trainer_create: out of device memory"); }
     // parameters, zero moments, trainable mask (BatchNorm running statistics are not parameters)
     std::vector<uint8_t> mask(T->np, 1);

@@ -324,6 +324,28 @@ def test_part_workgroup_convs_bit_identical(require_gpu, monkeypatch, blocks, n,
     assert np.array_equal(p1, p0), np.abs(p1 - p0).max()
 
 
+@pytest.mark.parametrize("blocks,n", [(2, 81), (2, 512), (3, 64), (2, 4)])
+def test_weight_grad_one_wave_per_simd_bit_identical(require_gpu, monkeypatch, blocks, n):
+    """Round 6: the default Winograd weight grad (wino_wgrad_gemm4_kernel: one wave per SIMD,
+    accumulators in AGPRs, the next board transformed and the one after loaded between single
+    MFMAs) against the 8-wave kernel (AZ_TRAIN_WGRAD4=0): the same MFMA sequence per accumulator
+    and the same transform operations, so two steps give bit-identical losses, gradients and
+    parameters.  n = 81: 14 splits of 6 boards, the last of 3; 64: 16 splits of 4 boards (a world-8
+    shard); 4: splits of one board."""
+    w = A.random_weights(blocks, 256, seed=19)
+    planes, tpol, tval = batch(n, seed=400 + n)
+    out = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("AZ_TRAIN_WGRAD4", flag)
+        tr = A.Trainer(blocks, 256, weights=w, max_batch=n)
+        losses = [tr.step(planes, tpol, tval, A.get_cyclical_lr(it)) for it in range(2)]
+        out[flag] = (losses, tr.grads(), tr.params())
+    (l1, g1, p1), (l0, g0, p0) = out["1"], out["0"]
+    assert l1 == l0
+    assert np.array_equal(g1, g0), np.abs(g1 - g0).max()
+    assert np.array_equal(p1, p0), np.abs(p1 - p0).max()
+
+
 def test_winograd_weight_grad_multi_split(require_gpu):
     """the production Winograd weight grad (wino_wgrad_gemm_kernel, at most 16 splits of
     whole boards, summed by wino_wgrad_reduce_out_kernel) with a partial last split: 81 boards =
