@@ -1151,6 +1151,11 @@ conv_wino_train_kernel(const float* __restrict__ X, const uint4* __restrict__ U,
             tr[5] = (unsigned)__builtin_amdgcn_s_getreg(20 | (31 << 11));
         }
 #endif
+        // (Round 6: the next board's XIN 1 staging beside this board's MFMAs -- one float4 per thread
+        // per input chunk, after that chunk's transform, through a per-step hook in wino_core --
+        // was bit-identical and measured 21.26 vs 21.15 ms per step: the BatchNorm apply's IEEE
+        // divisions cost the MFMA waves more than the staging phase they replaced, and only every
+        // second board's staging can move.  profiles/r06w_ab_prestage_b512.txt; not kept.)
         if constexpr (XIN == 1) {   // thread = channel quad tid % 64 (F / 4 = 64 divides 512) x rows tid / 64 + 8 k
             static_assert(F / 4 == 64, "BNIN staging assumes 64 channel quads");
             const int cq = tid & 63;
