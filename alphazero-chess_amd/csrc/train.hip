@@ -411,9 +411,9 @@ __device__ __forceinline__ void static_for(Fn&& f) { static_for_impl(f, std::mak
 // four adds.  Every accumulator gets the same MFMA sequence as in wino_wgrad_gemm_kernel (rows in
 // order, four per MFMA) and the transforms the same operations: the partials are bit-identical
 // (test_weight_grad_one_wave_per_simd_bit_identical).  Measured at B = 512
-// (profiles/r06s_*): 148.6 us against 164-168 us, and 130.9 us with the side jobs removed (a
-// pricing build, wrong results): the transforms and loads cost the one MFMA wave ~12 %, which
-// fillers of 16-24 cycles per 32-cycle f32 MFMA gap do not hide.
+// (profiles/r06u_ab_wgrad4_b512.txt, r06o_wgrad_pricing.txt): 148.6 us against 164-168 us, and
+// 130.9 us with the side jobs removed (a pricing build, wrong results): the transforms and loads
+// cost the one MFMA wave ~12 %, which fillers of 16-24 cycles per 32-cycle f32 MFMA gap do not hide.
 template <int R, int Q>
 __device__ __forceinline__ void wgrad4_body(const float* __restrict__ X, const float* __restrict__ DY, int K,
                                             int rows_per_split, float* __restrict__ partial, float* xsm, float* dsm) {
