@@ -119,13 +119,14 @@ def cpu_baseline(blocks, filters, threads, games, sims, port=True):
     if not port:
         return out
     rnet = O.RefNet(blocks, filters, w)
-    pcfg = O.make_cfg(sims=max(sims // 4, 1), noise=True, seed=42, eval_kind=1, net=rnet, threads=threads)
+    psims = max(sims // 16, 1)
+    pcfg = O.make_cfg(sims=psims, noise=True, seed=42, eval_kind=1, net=rnet, threads=threads)
     t0 = time.perf_counter()
-    _, psims, _ = O.selfplay(pcfg, 16, max_plies=1)
+    _, pdone, _ = O.selfplay(pcfg, 16, max_plies=1)
     pdt = time.perf_counter() - t0
-    out["per_game_port"] = {"value": psims / pdt, "unit": "sims/s", "threads": threads,
+    out["per_game_port"] = {"value": pdone / pdt, "unit": "sims/s", "threads": threads,
                             "sample": "16 games x 1 move x %d sims, one leaf per game at a time, naive C "
-                                      "convolution (oracle/net_ref.c), %.1f s" % (max(sims // 4, 1), pdt)}
+                                      "convolution (oracle/net_ref.c), %.1f s" % (psims, pdt)}
     return out
 
 
@@ -453,7 +454,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-games", type=int, default=64)
-    ap.add_argument("--cpu-sims", type=int, default=32, help="sims per sampled search (batched leg ~10 s of host work at 20x256)")
+    ap.add_argument("--cpu-sims", type=int, default=160, help="sims per sampled search (batched leg ~8 s of host work at 20x256 on 16 threads)")
     ap.add_argument("--train-steps", type=int, default=5, help="timed training steps (0 = skip the training phase)")
     ap.add_argument("--train-batch", type=int, default=512, help="positions per rank (BATCH_SIZE, parameters.rs:17)")
     ap.add_argument("--train-timeout", type=int, default=90)
