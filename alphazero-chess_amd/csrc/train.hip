@@ -414,16 +414,19 @@ __device__ __forceinline__ void static_for(Fn&& f) { static_for_impl(f, std::mak
 // (profiles/r06u_ab_wgrad4_b512.txt, r06o_wgrad_pricing.txt): 148.6 us against 164-168 us, and
 // 130.9 us with the side jobs removed (a pricing build, wrong results): the transforms and loads
 // cost the one MFMA wave ~12 %, which fillers of 16-24 cycles per 32-cycle f32 MFMA gap do not hide.
-template <int R, int Q>
+template <int R, int Q, int NQ>
 __device__ __forceinline__ void wgrad4_body(const float* __restrict__ X, const float* __restrict__ DY, int K,
                                             int rows_per_split, float* __restrict__ partial, float* xsm, float* dsm) {
-    constexpr int NWV = 4, F = 256, CO = F / NWV, NN = CO / 16, TPT = 16 / NWV;
+    // NQ output-channel parts per (split, point): the workgroup owns co [FQ z, FQ z + FQ) (blockIdx.z)
+    constexpr int NWV = 4, F = 256, FQ = F / NQ, CO = FQ / NWV, NN = CO / 16, TPT = 16 / NWV;
+    constexpr int MQ = FQ / 4, MIT = 16 * MQ / 256;   // M' items (tile, co quad) per thread: 4 / NQ
     constexpr int XB = 16 * WG_SX, DB = 16 * WG_SD;   // one LDS buffer of V / M' rows
     constexpr int I1 = R == 0 ? 0 : 1, I2 = R == 3 ? 3 : 2, J1 = Q == 0 ? 0 : 1, J2 = Q == 3 ? 3 : 2;
     constexpr float RA = R == 3 ? 0.0f : 1.0f, RB = R == 0 ? 0.0f : (R == 1 ? 1.0f : -1.0f);
     constexpr float QA = Q == 3 ? 0.0f : 1.0f, QB = Q == 0 ? 0.0f : (Q == 1 ? 1.0f : -1.0f);
+    static_assert(NN >= 1 && MIT >= 1 && 4 % MIT == 0, "co parts");
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int split = blockIdx.x;
+    const int split = blockIdx.x, cob = FQ * (int)blockIdx.z;
     const int rbeg = split * rows_per_split, rend = min(K, rbeg + rows_per_split), nbd = (rend - rbeg) >> 4;
     f32x4 acc[16][NN];
 #pragma unroll
@@ -435,55 +438,73 @@ __device__ __forceinline__ void wgrad4_body(const float* __restrict__ X, const f
     const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, xbytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rD = __builtin_amdgcn_make_buffer_rsrc((void*)DY, (short)0, xbytes, 0x00020000);
     constexpr int OFF_BOARD = 0x40000000;
-    f32x4 xd[TPT][2][2], yv[TPT][2][2];
-    // wino_comb and the M' combination of wino_wgrad_gemm_kernel with the point's constants, in six
-    // steps of four floats (so that one step fits beside one MFMA)
-    f32x4 t1[TPT], t2[TPT], p0[TPT], p1[TPT];
-    auto xstep = [&](int buf, int u, int st) {
+    f32x4 xd[TPT][2][2], yv[MIT][2][2];
+    // wino_comb and the M' combination of wino_wgrad_gemm_kernel with the point's constants, in
+    // steps of four floats (so that one step fits beside one MFMA): V of tile u (the thread's
+    // channel quad lane of all 256 input channels), M' of item m (tile (tid + 256 m) / MQ, output
+    // channel quad (tid + 256 m) % MQ of the workgroup's FQ)
+    f32x4 t1[TPT], t2[TPT], p0[MIT], p1[MIT];
+    auto vstep = [&](int buf, int u, int st) {
         const int t = TPT * tp + u;
         if (st == 0) t1[u] = wino_comb(R, xd[u][0][0], xd[u][1][0]);
         if (st == 1) t2[u] = wino_comb(R, xd[u][0][1], xd[u][1][1]);
         if (st == 2) *reinterpret_cast<f32x4*>(xsm + buf * XB + t * WG_SX + c4) = wino_comb(Q, t1[u], t2[u]);
-        if (st == 3) p0[u] = yv[u][0][0] * RA + yv[u][1][0] * RB;
-        if (st == 4) p1[u] = yv[u][0][1] * RA + yv[u][1][1] * RB;
-        if (st == 5) *reinterpret_cast<f32x4*>(dsm + buf * DB + t * WG_SD + c4) = p0[u] * QA + p1[u] * QB;
     };
-    auto xform_tile = [&](int buf, int u) {
-#pragma unroll
-        for (int st = 0; st < 6; st++) xstep(buf, u, st);
+    auto mstep = [&](int buf, int m, int st) {
+        const int idx = tid + 256 * m, t = idx / MQ, cq = idx % MQ;
+        if (st == 0) p0[m] = yv[m][0][0] * RA + yv[m][1][0] * RB;
+        if (st == 1) p1[m] = yv[m][0][1] * RA + yv[m][1][1] * RB;
+        if (st == 2) *reinterpret_cast<f32x4*>(dsm + buf * DB + t * WG_SD + 4 * cq) = p0[m] * QA + p1[m] * QB;
     };
-    // load i of tile u of board bi: X squares i = 0-3, dY squares 4-7 (bi >= nbd: zeros, no branch)
-    auto load1 = [&](int bi, int u, int i) {
+    // X square i (0-3) of tile u, dY square i (0-3) of item m, of board bi (bi >= nbd: zeros, no branch)
+    auto loadx = [&](int bi, int u, int i) {
         const bool inb = bi < nbd;
         const int bb0 = inb ? ((rbeg >> 4) + bi) * 64 * F * 4 : 0, vin = inb ? c4 * 4 : OFF_BOARD;
         const int t = TPT * tp + u, ty = t >> 2, tx = t & 3;
-        if (i < 4) {
-            const int ii = i >> 1, jj = i & 1;
-            const int row = 2 * ty - 1 + (ii ? I2 : I1), col = 2 * tx - 1 + (jj ? J2 : J1);
-            const bool on = (unsigned)row < 8u && (unsigned)col < 8u;
-            xd[u][ii][jj] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                          rX, on ? vin : OFF_BOARD, on ? bb0 + (row * 8 + col) * F * 4 : 0, 0));
-        } else {
-            const int a = (i - 4) >> 1, bb = i & 1;
-            yv[u][a][bb] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                         rD, vin, bb0 + ((2 * ty + a) * 8 + 2 * tx + bb) * F * 4, 0));
-        }
+        const int ii = i >> 1, jj = i & 1;
+        const int row = 2 * ty - 1 + (ii ? I2 : I1), col = 2 * tx - 1 + (jj ? J2 : J1);
+        const bool on = (unsigned)row < 8u && (unsigned)col < 8u;
+        xd[u][ii][jj] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                      rX, on ? vin : OFF_BOARD, on ? bb0 + (row * 8 + col) * F * 4 : 0, 0));
+    };
+    auto loady = [&](int bi, int m, int i) {
+        const bool inb = bi < nbd;
+        const int idx = tid + 256 * m, t = idx / MQ, cq = idx % MQ, ty = t >> 2, tx = t & 3;
+        const int a = i >> 1, bb = i & 1;
+        const int bb0 = inb ? ((rbeg >> 4) + bi) * 64 * F * 4 : 0;
+        const int vo = inb ? (((2 * ty + a) * 8 + 2 * tx + bb) * F + cob + 4 * cq) * 4 : OFF_BOARD;
+        yv[m][a][bb] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rD, vo, bb0, 0));
     };
     if (nbd > 0) {
 #pragma unroll
-        for (int u = 0; u < TPT; u++)
+        for (int i = 0; i < 4; i++) {
 #pragma unroll
-            for (int i = 0; i < 8; i++) load1(0, u, i);
+            for (int u = 0; u < TPT; u++) loadx(0, u, i);
 #pragma unroll
-        for (int u = 0; u < TPT; u++) xform_tile(0, u);
+            for (int m = 0; m < MIT; m++) loady(0, m, i);
+        }
 #pragma unroll
-        for (int u = 0; u < TPT; u++)
+        for (int st = 0; st < 3; st++) {
 #pragma unroll
-            for (int i = 0; i < 8; i++) load1(1, u, i);
+            for (int u = 0; u < TPT; u++) vstep(0, u, st);
+#pragma unroll
+            for (int m = 0; m < MIT; m++) mstep(0, m, st);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+#pragma unroll
+            for (int u = 0; u < TPT; u++) loadx(1, u, i);
+#pragma unroll
+            for (int m = 0; m < MIT; m++) loady(1, m, i);
+        }
     }
     __syncthreads();
     float bv[2][NN];
     f32x4 av[2][4];
+    // side-job slots in a row quad of 16 NN MFMAs: the transform steps at k = 0, 2, .., 10, then
+    // the eight loads LS MFMAs apart from k = L0 (a load costs the issuing wave more than one MFMA
+    // gap, so they are spread over the quad)
+    constexpr int L0 = NN >= 4 ? 16 : 12, LS = NN >= 4 ? 6 : 2;
     for (int b = 0; b < nbd; b++) {
         const int cur = b & 1, nxt = cur ^ 1;
         auto rd = [&](int qq) {
@@ -493,14 +514,17 @@ __device__ __forceinline__ void wgrad4_body(const float* __restrict__ X, const f
 #pragma unroll
             for (int j = 0; j < 4; j++) av[o][j] = *reinterpret_cast<const f32x4*>(xsm + cur * XB + rq * WG_SX + 64 * j + 4 * (lane & 15));
         };
-        // side jobs beside the MFMAs of row quad u (k = its MFMA index, 0..63): the six transform
-        // steps of board b + 1's tile u at k = 0, 2, .., 10, then board b + 2's eight loads of
-        // that tile into the registers just freed, six MFMAs apart from k = 16 (a load costs the
-        // issuing wave more than one MFMA gap, so they are spread over the board)
+        // beside row quad u: board b + 1's V of tile u and M' of item u / (4 / MIT) (in the quads
+        // u % (4 / MIT) == 0), then board b + 2's loads of them into the registers just freed
         auto side = [&](auto U, auto KK) {
             constexpr int u = decltype(U)::value, k = decltype(KK)::value;
-            if constexpr (k <= 10 && k % 2 == 0) xstep(nxt, u, k / 2);
-            if constexpr (k >= 16 && (k - 16) % 6 == 0 && (k - 16) / 6 < 8) load1(b + 2, u, (k - 16) / 6);
+            constexpr bool hasm = u % (4 / MIT) == 0;
+            constexpr int m = u / (4 / MIT);
+            if constexpr (k <= 4 && k % 2 == 0) vstep(nxt, u, k / 2);
+            if constexpr (hasm && k >= 6 && k <= 10 && k % 2 == 0) mstep(nxt, m, (k - 6) / 2);
+            if constexpr (k >= L0 && (k - L0) % LS == 0 && (k - L0) / LS < 4) loadx(b + 2, u, (k - L0) / LS);
+            if constexpr (hasm && k >= L0 && (k - L0) % LS == 0 && (k - L0) / LS >= 4 && (k - L0) / LS < 8)
+                loady(b + 2, m, (k - L0) / LS - 4);
         };
         rd(0);
         static_for<16>([&](auto G) {
@@ -511,9 +535,9 @@ __device__ __forceinline__ void wgrad4_body(const float* __restrict__ X, const f
             if constexpr (g == 8) rd(3);
             __builtin_amdgcn_sched_barrier(0);
             static_for<4 * NN>([&](auto CN) {
-                constexpr int c = decltype(CN)::value / NN, n = decltype(CN)::value % NN, k = 16 * j + 4 * c + n;
+                constexpr int c = decltype(CN)::value / NN, n = decltype(CN)::value % NN, k = 4 * NN * j + NN * c + n;
                 asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+a"(acc[4 * j + c][n]) : "v"(av[o][j][c]), "v"(bv[o][n]));
-                if constexpr ((k <= 10 && k % 2 == 0) || (k >= 16 && (k - 16) % 6 == 0 && (k - 16) / 6 < 8)) {
+                if constexpr ((k <= 10 && k % 2 == 0) || (k >= L0 && (k - L0) % LS == 0 && (k - L0) / LS < 8)) {
                     __builtin_amdgcn_sched_barrier(0);
                     side(std::integral_constant<int, qq>{}, std::integral_constant<int, k>{});
                     __builtin_amdgcn_sched_barrier(0);
@@ -534,16 +558,17 @@ __device__ __forceinline__ void wgrad4_body(const float* __restrict__ X, const f
             for (int n = 0; n < NN; n++)
 #pragma unroll
                 for (int g = 0; g < 4; g++) {
-                    const int ci = 64 * j + 4 * (4 * (lane >> 4) + g) + c, co = CO * w + 16 * n + (lane & 15);
+                    const int ci = 64 * j + 4 * (4 * (lane >> 4) + g) + c, co = cob + CO * w + 16 * n + (lane & 15);
                     out[(size_t)ci * F + co] = acc[4 * j + c][n][g];
                 }
 }
+template <int NQ>
 __global__ void __launch_bounds__(256)
 wino_wgrad_gemm4_kernel(const float* __restrict__ X, const float* __restrict__ DY, int K, int rows_per_split,
                         float* __restrict__ partial) {
     __shared__ __attribute__((aligned(16))) float xs[2 * 16 * WG_SX];
     __shared__ __attribute__((aligned(16))) float ds[2 * 16 * WG_SD];
-#define AZ_WG4(x) case x: wgrad4_body<((x) / 4), ((x) % 4)>(X, DY, K, rows_per_split, partial, xs, ds); break;
+#define AZ_WG4(x) case x: wgrad4_body<((x) / 4), ((x) % 4), NQ>(X, DY, K, rows_per_split, partial, xs, ds); break;
     switch (blockIdx.y) {
         AZ_WG4(0) AZ_WG4(1) AZ_WG4(2) AZ_WG4(3) AZ_WG4(4) AZ_WG4(5) AZ_WG4(6) AZ_WG4(7)
         AZ_WG4(8) AZ_WG4(9) AZ_WG4(10) AZ_WG4(11) AZ_WG4(12) AZ_WG4(13) AZ_WG4(14) AZ_WG4(15)
@@ -1928,6 +1953,10 @@ struct Trainer {
     int half = -1;                           // conv workgroups per board at small batches: -1 auto (4 when 4B <= the CU
                                              // count, 2 when 2B <=), 0 one per board, 2 / 4 always (env AZ_TRAIN_HALF)
     bool wgrad4 = true;                      // weight grad with one wave per SIMD (env AZ_TRAIN_WGRAD4=0: the 8-wave kernel)
+    int wgrad_cosplit = 256;                 // batches up to this many boards split the one-wave weight grad's output
+                                             // channels over two workgroups (env AZ_TRAIN_WGRAD_COSPLIT; round 6:
+                                             // -4.5 / -3 / -0.8 % per step at 64 / 128 / 256, +0.7 % at 512)
+    int wgrad_rows = 0;                      // A/B: a fixed weight-grad split size in rows (env AZ_TRAIN_WGRAD_ROWS)
     // the conv bias gradients of the tower's BatchNorms: bn_back4 partials per BN, summed in one
     // launch at the end of the backward (bias_dst[j] = gradient offset of BN j's conv bias)
     float* bsum_all = nullptr;
@@ -2096,23 +2125,33 @@ int launch_wgrad(Trainer* T, int taps, const float* X, int ldx, int K, const flo
 // 64 positions per rank of a world-8 sharded step (64 rows per split; round 6 -- a fixed 512-row
 // split left 32 workgroups there, as slow as the whole 512 batch)
 constexpr int WINO_GEMM_SPLITS = 16;
-int g_wgrad_rows = 0;   // A/B only (env AZ_TRAIN_WGRAD_ROWS): a fixed split size in rows (round 5: 512)
-int wino_gemm_rows(int B) { return g_wgrad_rows > 0 ? g_wgrad_rows : 16 * ((B + WINO_GEMM_SPLITS - 1) / WINO_GEMM_SPLITS); }
-size_t wino_gemm_splits(int B) { return (size_t)((B * 16 + wino_gemm_rows(B) - 1) / wino_gemm_rows(B)); }
-size_t wino_gemm_splits_max(int Bmax) {   // over B <= Bmax
-    return g_wgrad_rows > 0 ? wino_gemm_splits(Bmax) : (size_t)std::min(Bmax, WINO_GEMM_SPLITS);
+// nq output-channel parts per (split, point) (wino_wgrad_gemm4_kernel<2> at small batches): 16 / nq
+// splits, so the workgroups stay 256 and the split partials shrink by nq.  fixed > 0 (A/B only, env
+// AZ_TRAIN_WGRAD_ROWS): a fixed split size in rows (round 5: 512)
+int wino_gemm_rows(int B, int nq, int fixed) {
+    const int S = WINO_GEMM_SPLITS / nq;
+    return fixed > 0 ? fixed : 16 * ((B + S - 1) / S);
+}
+size_t wino_gemm_splits(int B, int nq, int fixed) {
+    const int rows = wino_gemm_rows(B, nq, fixed);
+    return (size_t)((B * 16 + rows - 1) / rows);
+}
+size_t wino_gemm_splits_max(int Bmax, int fixed) {   // over B <= Bmax and nq
+    return fixed > 0 ? wino_gemm_splits(Bmax, 1, fixed) : (size_t)std::min(Bmax, WINO_GEMM_SPLITS);
 }
 int launch_wino_wgrad(Trainer* T, const float* X, const float* DY, int B, float* g) {
     const int F = T->F, K = B * 16;
     if (F != 256) return fail("Winograd wgrad: F = 256 only");
     if (B > T->Bmax) return fail("Winograd wgrad: batch too large");
-    const int splits = (int)wino_gemm_splits(B);
+    const int nq = T->wgrad4 && B <= T->wgrad_cosplit ? 2 : 1;
+    const int splits = (int)wino_gemm_splits(B, nq, T->wgrad_rows), rows = wino_gemm_rows(B, nq, T->wgrad_rows);
     if (splits * 16 * (size_t)F * F > T->wpart_cap) return fail("Winograd wgrad: partial buffer too small");
     if ((size_t)B * 64 * F * 4 >= (size_t)0x40000000) return fail("Winograd wgrad: batch too large for 32-bit offsets");
     if ((size_t)F * F % 256) return fail("Winograd wgrad: F * F must be a multiple of 256");
     const unsigned rblocks = (unsigned)((size_t)F * F / 256);
-    if (T->wgrad4) tr::wino_wgrad_gemm4_kernel<<<dim3(splits, 16), 256, 0, T->st>>>(X, DY, K, wino_gemm_rows(B), T->wpart);
-    else tr::wino_wgrad_gemm_kernel<<<dim3(splits, 16), 512, 0, T->st>>>(X, DY, K, wino_gemm_rows(B), T->wpart);
+    if (nq == 2) tr::wino_wgrad_gemm4_kernel<2><<<dim3(splits, 16, 2), 256, 0, T->st>>>(X, DY, K, rows, T->wpart);
+    else if (T->wgrad4) tr::wino_wgrad_gemm4_kernel<1><<<dim3(splits, 16), 256, 0, T->st>>>(X, DY, K, rows, T->wpart);
+    else tr::wino_wgrad_gemm_kernel<<<dim3(splits, 16), 512, 0, T->st>>>(X, DY, K, rows, T->wpart);
     tr::wino_wgrad_reduce_out_kernel<<<rblocks, 1024, 0, T->st>>>(T->wpart, splits, F, g);
     return hipGetLastError() == hipSuccess ? 0 : fail("Winograd wgrad launch failed");
 }
@@ -2812,9 +2851,9 @@ int az_trainer_create(int blocks, int filters, const float* weights, size_t n, i
     wp = std::max(wp, s1 * (size_t)F * 64);                             // heads 1x1
     wp = std::max(wp, s1 * 32 * 64);                                    // policy_conv_2
     wp = std::max(wp, sl * 512 * 64);                                   // value_linear_1
-    if (const char* e = getenv("AZ_TRAIN_WGRAD_ROWS")) g_wgrad_rows = std::max(0, atoi(e) / 16 * 16);
+    if (const char* e = getenv("AZ_TRAIN_WGRAD_ROWS")) T->wgrad_rows = std::max(0, atoi(e) / 16 * 16);
     if (T->wino) {   // Winograd weight grads: [16][Bmax * 16][F] transforms, dU [16][F][F]
-        wp = std::max(wp, wino_gemm_splits_max(max_batch) * 16 * (size_t)F * F);
+        wp = std::max(wp, wino_gemm_splits_max(max_batch, T->wgrad_rows) * 16 * (size_t)F * F);
     }
     T->wpart_cap = wp;
     T->wpart = A(wp);
@@ -2842,6 +2881,7 @@ int az_trainer_create(int blocks, int filters, const float* weights, size_t n, i
     if (const char* e = getenv("AZ_TRAIN_ORC")) T->orc = atoi(e) != 0;
     if (const char* e = getenv("AZ_TRAIN_HALF")) T->half = atoi(e);
     if (const char* e = getenv("AZ_TRAIN_WGRAD4")) T->wgrad4 = atoi(e) != 0;
+    if (const char* e = getenv("AZ_TRAIN_WGRAD_COSPLIT")) T->wgrad_cosplit = atoi(e);
     if (!ok) { delete T; return fail("az_trainer_create: out of device memory"); }
     // parameters, zero moments, trainable mask (BatchNorm running statistics are not parameters)
     std::vector<uint8_t> mask(T->np, 1);

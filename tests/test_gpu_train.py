@@ -346,6 +346,28 @@ def test_weight_grad_one_wave_per_simd_bit_identical(require_gpu, monkeypatch, b
     assert np.array_equal(p1, p0), np.abs(p1 - p0).max()
 
 
+@pytest.mark.parametrize("blocks,n,rows", [(2, 64, 128), (3, 81, 176), (2, 4, 16)])
+def test_weight_grad_output_channel_split_bit_identical(require_gpu, monkeypatch, blocks, n, rows):
+    """Round 6: the one-wave weight grad with its output channels split over two workgroups
+    (wino_wgrad_gemm4_kernel<2>, AZ_TRAIN_WGRAD_COSPLIT: half the split partials at small batches)
+    against one workgroup per (split, point), at the same split size (AZ_TRAIN_WGRAD_ROWS): each
+    output channel's accumulator takes the same MFMAs in the same order, so two steps give
+    bit-identical losses, gradients and parameters."""
+    w = A.random_weights(blocks, 256, seed=29)
+    planes, tpol, tval = batch(n, seed=600 + n)
+    monkeypatch.setenv("AZ_TRAIN_WGRAD_ROWS", str(rows))
+    out = {}
+    for flag in (str(n), "0"):
+        monkeypatch.setenv("AZ_TRAIN_WGRAD_COSPLIT", flag)
+        tr = A.Trainer(blocks, 256, weights=w, max_batch=n)
+        losses = [tr.step(planes, tpol, tval, A.get_cyclical_lr(it)) for it in range(2)]
+        out[flag] = (losses, tr.grads(), tr.params())
+    (l1, g1, p1), (l0, g0, p0) = out[str(n)], out["0"]
+    assert l1 == l0
+    assert np.array_equal(g1, g0), np.abs(g1 - g0).max()
+    assert np.array_equal(p1, p0), np.abs(p1 - p0).max()
+
+
 def test_winograd_weight_grad_multi_split(require_gpu):
     """the production Winograd weight grad (wino_wgrad_gemm_kernel, at most 16 splits of
     whole boards, summed by wino_wgrad_reduce_out_kernel) with a partial last split: 81 boards =

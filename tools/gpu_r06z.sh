@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round 6: the weight grad's output channels split over two workgroups at small batches
+# (AZ_TRAIN_WGRAD_COSPLIT): bit-identity, one-wave identity, A/B at 64 / 128 / 256 positions
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+timeout -k 10 400 python -u -m pytest tests/test_gpu_train.py -x -v --timeout 200 --timeout-method thread -k "channel_split or one_wave or multi_split or oracle" > gpurun_out/r06z_tests.log 2>&1 || { echo "tests failed"; exit 1; }
+for b in 64 128 256; do
+  timeout -k 10 300 python -u tools/train_ab.py $b 10 3 "cs:AZ_TRAIN_WGRAD_COSPLIT=$b" 'one:AZ_TRAIN_WGRAD_COSPLIT=0' > gpurun_out/r06z_ab_b$b.txt 2>&1 || { echo "ab $b failed"; exit 1; }
+done
+cd /tmp && export TMPDIR=/tmp
+AZ_TRAIN_WGRAD_COSPLIT=64 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/r06z_prof64 -o t -- python3 $GRAFT_REPO_ROOT/tools/train_prof.py 4 64 > $GRAFT_REPO_ROOT/gpurun_out/r06z_prof64.log 2>&1 || exit 1
+echo r06z-ok
