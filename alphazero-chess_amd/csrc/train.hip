@@ -501,10 +501,11 @@ __device__ __forceinline__ void wgrad4_body(const float* __restrict__ X, const f
     __syncthreads();
     float bv[2][NN];
     f32x4 av[2][4];
-    // side-job slots in a row quad of 16 NN MFMAs: the transform steps at k = 0, 2, .., 10, then
-    // the eight loads LS MFMAs apart from k = L0 (a load costs the issuing wave more than one MFMA
-    // gap, so they are spread over the quad)
-    constexpr int L0 = NN >= 4 ? 16 : 12, LS = NN >= 4 ? 6 : 2;
+    // side-job slots in a row quad of 16 NN MFMAs: the V steps VS MFMAs apart from k = 0, the M'
+    // steps from k = 3 VS, then the eight loads LS MFMAs apart from k = L0 (a load costs the issuing
+    // wave more than one MFMA gap, so they are spread over the quad)
+    constexpr int VS = NN >= 2 ? 2 : 1, L0 = NN >= 4 ? 16 : NN == 2 ? 12 : 6, LS = NN >= 4 ? 6 : NN == 2 ? 2 : 1;
+    static_assert(L0 + 7 * LS < 16 * NN && 6 * VS <= L0, "side-job slots fit the quad");
     for (int b = 0; b < nbd; b++) {
         const int cur = b & 1, nxt = cur ^ 1;
         auto rd = [&](int qq) {
@@ -520,8 +521,8 @@ __device__ __forceinline__ void wgrad4_body(const float* __restrict__ X, const f
             constexpr int u = decltype(U)::value, k = decltype(KK)::value;
             constexpr bool hasm = u % (4 / MIT) == 0;
             constexpr int m = u / (4 / MIT);
-            if constexpr (k <= 4 && k % 2 == 0) vstep(nxt, u, k / 2);
-            if constexpr (hasm && k >= 6 && k <= 10 && k % 2 == 0) mstep(nxt, m, (k - 6) / 2);
+            if constexpr (k < 3 * VS && k % VS == 0) vstep(nxt, u, k / VS);
+            if constexpr (hasm && k >= 3 * VS && k < 6 * VS && k % VS == 0) mstep(nxt, m, (k - 3 * VS) / VS);
             if constexpr (k >= L0 && (k - L0) % LS == 0 && (k - L0) / LS < 4) loadx(b + 2, u, (k - L0) / LS);
             if constexpr (hasm && k >= L0 && (k - L0) % LS == 0 && (k - L0) / LS >= 4 && (k - L0) / LS < 8)
                 loady(b + 2, m, (k - L0) / LS - 4);
@@ -537,7 +538,7 @@ __device__ __forceinline__ void wgrad4_body(const float* __restrict__ X, const f
             static_for<4 * NN>([&](auto CN) {
                 constexpr int c = decltype(CN)::value / NN, n = decltype(CN)::value % NN, k = 4 * NN * j + NN * c + n;
                 asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+a"(acc[4 * j + c][n]) : "v"(av[o][j][c]), "v"(bv[o][n]));
-                if constexpr ((k <= 10 && k % 2 == 0) || (k >= L0 && (k - L0) % LS == 0 && (k - L0) / LS < 8)) {
+                if constexpr ((k < 6 * VS && k % VS == 0) || (k >= L0 && (k - L0) % LS == 0 && (k - L0) / LS < 8)) {
                     __builtin_amdgcn_sched_barrier(0);
                     side(std::integral_constant<int, qq>{}, std::integral_constant<int, k>{});
                     __builtin_amdgcn_sched_barrier(0);
@@ -1957,6 +1958,8 @@ struct Trainer {
                                              // channels over two workgroups (env AZ_TRAIN_WGRAD_COSPLIT; round 6:
                                              // -4.5 / -3 / -0.8 % per step at 64 / 128 / 256, +0.7 % at 512)
     int wgrad_rows = 0;                      // A/B: a fixed weight-grad split size in rows (env AZ_TRAIN_WGRAD_ROWS)
+    int wgrad_cosplit4 = 64;                 // ... and up to this many over four (env AZ_TRAIN_WGRAD_COSPLIT4; round 6: -0.9 %
+                                             // at 64 against two, +1.5 % at 128)
     // the conv bias gradients of the tower's BatchNorms: bn_back4 partials per BN, summed in one
     // launch at the end of the backward (bias_dst[j] = gradient offset of BN j's conv bias)
     float* bsum_all = nullptr;
@@ -2143,13 +2146,14 @@ int launch_wino_wgrad(Trainer* T, const float* X, const float* DY, int B, float*
     const int F = T->F, K = B * 16;
     if (F != 256) return fail("Winograd wgrad: F = 256 only");
     if (B > T->Bmax) return fail("Winograd wgrad: batch too large");
-    const int nq = T->wgrad4 && B <= T->wgrad_cosplit ? 2 : 1;
+    const int nq = !T->wgrad4 ? 1 : B <= T->wgrad_cosplit4 ? 4 : B <= T->wgrad_cosplit ? 2 : 1;
     const int splits = (int)wino_gemm_splits(B, nq, T->wgrad_rows), rows = wino_gemm_rows(B, nq, T->wgrad_rows);
     if (splits * 16 * (size_t)F * F > T->wpart_cap) return fail("Winograd wgrad: partial buffer too small");
     if ((size_t)B * 64 * F * 4 >= (size_t)0x40000000) return fail("Winograd wgrad: batch too large for 32-bit offsets");
     if ((size_t)F * F % 256) return fail("Winograd wgrad: F * F must be a multiple of 256");
     const unsigned rblocks = (unsigned)((size_t)F * F / 256);
-    if (nq == 2) tr::wino_wgrad_gemm4_kernel<2><<<dim3(splits, 16, 2), 256, 0, T->st>>>(X, DY, K, rows, T->wpart);
+    if (nq == 4) tr::wino_wgrad_gemm4_kernel<4><<<dim3(splits, 16, 4), 256, 0, T->st>>>(X, DY, K, rows, T->wpart);
+    else if (nq == 2) tr::wino_wgrad_gemm4_kernel<2><<<dim3(splits, 16, 2), 256, 0, T->st>>>(X, DY, K, rows, T->wpart);
     else if (T->wgrad4) tr::wino_wgrad_gemm4_kernel<1><<<dim3(splits, 16), 256, 0, T->st>>>(X, DY, K, rows, T->wpart);
     else tr::wino_wgrad_gemm_kernel<<<dim3(splits, 16), 512, 0, T->st>>>(X, DY, K, rows, T->wpart);
     tr::wino_wgrad_reduce_out_kernel<<<rblocks, 1024, 0, T->st>>>(T->wpart, splits, F, g);
@@ -2882,6 +2886,7 @@ int az_trainer_create(int blocks, int filters, const float* weights, size_t n, i
     if (const char* e = getenv("AZ_TRAIN_HALF")) T->half = atoi(e);
     if (const char* e = getenv("AZ_TRAIN_WGRAD4")) T->wgrad4 = atoi(e) != 0;
     if (const char* e = getenv("AZ_TRAIN_WGRAD_COSPLIT")) T->wgrad_cosplit = atoi(e);
+    if (const char* e = getenv("AZ_TRAIN_WGRAD_COSPLIT4")) T->wgrad_cosplit4 = atoi(e);
     if (!ok) { delete T; return fail("az_trainer_create: out of device memory"); }
     // parameters, zero moments, trainable mask (BatchNorm running statistics are not parameters)
     std::vector<uint8_t> mask(T->np, 1);

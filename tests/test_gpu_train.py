@@ -348,19 +348,22 @@ def test_weight_grad_one_wave_per_simd_bit_identical(require_gpu, monkeypatch, b
     assert np.array_equal(p1, p0), np.abs(p1 - p0).max()
 
 
+@pytest.mark.parametrize("parts", ["AZ_TRAIN_WGRAD_COSPLIT", "AZ_TRAIN_WGRAD_COSPLIT4"])
 @pytest.mark.parametrize("blocks,n,rows", [(2, 64, 128), (3, 81, 176), (2, 4, 16)])
-def test_weight_grad_output_channel_split_bit_identical(require_gpu, monkeypatch, blocks, n, rows):
-    """Round 6: the one-wave weight grad with its output channels split over two workgroups
-    (wino_wgrad_gemm4_kernel<2>, AZ_TRAIN_WGRAD_COSPLIT: half the split partials at small batches)
-    against one workgroup per (split, point), at the same split size (AZ_TRAIN_WGRAD_ROWS): each
+def test_weight_grad_output_channel_split_bit_identical(require_gpu, monkeypatch, blocks, n, rows, parts):
+    """Round 6: the one-wave weight grad with its output channels split over two or four
+    workgroups (wino_wgrad_gemm4_kernel<2> / <4>, AZ_TRAIN_WGRAD_COSPLIT / _COSPLIT4: half / a quarter
+    of the split partials at small batches) against one workgroup per (split, point), at the same
+    split size (AZ_TRAIN_WGRAD_ROWS): each
     output channel's accumulator takes the same MFMAs in the same order, so two steps give
     bit-identical losses, gradients and parameters."""
     w = A.random_weights(blocks, 256, seed=29)
     planes, tpol, tval = batch(n, seed=600 + n)
     monkeypatch.setenv("AZ_TRAIN_WGRAD_ROWS", str(rows))
+    monkeypatch.setenv("AZ_TRAIN_WGRAD_COSPLIT", "0")
     out = {}
     for flag in (str(n), "0"):
-        monkeypatch.setenv("AZ_TRAIN_WGRAD_COSPLIT", flag)
+        monkeypatch.setenv(parts, flag)
         tr = A.Trainer(blocks, 256, weights=w, max_batch=n)
         losses = [tr.step(planes, tpol, tval, A.get_cyclical_lr(it)) for it in range(2)]
         out[flag] = (losses, tr.grads(), tr.params())
