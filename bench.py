@@ -447,6 +447,8 @@ def main():
     ap.add_argument("--filters", type=int, default=256)
     ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"],
                     help="headline precision (the reference computes in f32)")
+    ap.add_argument("--c2-steps", type=int, default=20,
+                    help="moves (800 sims each) of the C2 steady-state leg: 256 games x 6x64 f32 (0 = skip)")
     ap.add_argument("--bf16-steps", type=int, default=-1,
                     help="steps of the labelled bf16_mode leg (-1 = same as --steps, 0 = skip)")
     ap.add_argument("--cache", type=int, default=0,
@@ -523,17 +525,19 @@ def main():
         dist_barrier(world)
         synchronize()
 
-    def phase(net, cache, steps, timing):
+    def phase(net, cache, steps, timing, G=G, S=S, K=K, warmup=None):
         """Self-play from startpos: warmup steps, then `steps` timed steps of K simulation steps; with
         `timing`, every 32nd simulation step carries HIP events (roofline / tree_walk), in the window
-        or in a profile pass after it (persistent kernel)."""
+        or in a profile pass after it (persistent kernel).  G / S / K: the workload (default the
+        headline's)."""
+        warmup = args.warmup if warmup is None else warmup
         if args.rehearse:
             sp = RehearsalSelfPlay(G, S, sh["seed"])
         else:
             sp = A.SelfPlay(net, games=G, sims=S, device=local, continuous=True, seed=sh["seed"],
                             cache_capacity=cache)
         sp.reset()
-        for _ in range(args.warmup):
+        for _ in range(warmup):
             sp.run_sims(K)
             sp.drain()
         st0 = sp.search.stats()
@@ -581,7 +585,7 @@ def main():
         res["rank_root_digests"] = digests
         return elapsed, res, tm, c[0]
 
-    def roofline(tm, dtype, net):
+    def roofline(tm, dtype, net, B=args.blocks, Fh=args.filters, G=G):
         """The fused tower over the timed region (HIP events around its launch on the engine stream,
         every 32nd simulation step).  achieved / frac = the MFMA FLOPs the kernel EXECUTES per launch
         (what the matrix pipe does: SURVEY 8d's roofline for the tower) / its measured time vs the
@@ -592,11 +596,10 @@ def main():
         traffic_ratio = traffic / the algorithmic bytes (every weight once + the rows' I/O)."""
         peak = PEAK_BF16_TFLOPS if dtype == "bf16" else PEAK_F32_TFLOPS
         launches = max(tm["conv_launches"], 1)
-        rows = tm["conv_flop"] / max(tower_algo_flop_per_row(args.blocks, args.filters), 1.0)
+        rows = tm["conv_flop"] / max(tower_algo_flop_per_row(B, Fh), 1.0)
         secs = tm["conv_ms"] * 1e-3
         kname = net.tower_kernel if net is not None else "none (rehearsal)"
         wino = net is not None and net.winograd
-        B, Fh = args.blocks, args.filters
         exec_row = tower_exec_flop_per_row(B, Fh, dtype, wino or net is None)
         exec_tflops = exec_row * rows / secs / 1e12 if secs > 0 else 0.0
         algo_tflops = tm["conv_flop"] / secs / 1e12 if secs > 0 else 0.0
@@ -661,6 +664,23 @@ def main():
                             "reported beside the headline, not as it"}
         del net16
         legs["bf16_mode"] = time.perf_counter() - tl
+
+    # C2 (BASELINE.json configs[1]) in steady state: 256 continuous games x 800 sims, 6x64 f32 net --
+    # the persistent per-game kernel (one game per CU), its tower timed in a profile pass after
+    # the window; beside games_per_hr_measured, which plays C2's games to the end
+    c2_res = None
+    if args.c2_steps > 0 and args.dtype == "f32":
+        tl = time.perf_counter()
+        net2 = None if args.rehearse else A.AlphaZero(6, 64, dtype="f32", device=local, seed=42)
+        e2, t2, tm2, _ = phase(net2, 0, args.c2_steps, True, G=256, S=800, K=800, warmup=2)
+        c2_res = {"value": t2["sims"] / e2, "unit": "sims/s", "n_gpus": world, "steps": args.c2_steps,
+                  "sims_per_step": 800, "ms_per_step": e2 / args.c2_steps * 1e3, "dtype": "f32",
+                  "config": "C2 (BASELINE.json configs[1]): 256 games/GPU x 800 sims/move, 6x64 f32 net, "
+                            "continuous self-play from startpos (one move of every game per step)",
+                  "evals_per_sim": t2["evals"] / max(t2["sims"], 1),
+                  "roofline": roofline(tm2, "f32", net2, 6, 64, 256)}
+        del net2
+        legs["c2_steady"] = time.perf_counter() - tl
 
     # the reference's FEN cache (tree.rs:214-219) on the same window, on request
     cache_res = None
@@ -760,6 +780,7 @@ def main():
         # games/hr measurement: see games_per_hr_measured / _projected
         "games_per_hr": None,
         "games_per_hr_measured": games_leg,
+        "c2_steady": c2_res,
         "rank_root_digests": tot["rank_root_digests"],
         "games_per_hr_projected": None,
         "cpu_baseline": None,
