@@ -14,7 +14,9 @@ sharded (different seeds), no collective on the path; barrier + max-over-ranks t
 Extra JSON fields: roofline (the fused tower kernel vs the f32 MFMA peak, HIP events on the
 engine stream over the timed region), bf16_mode (the same window with the bf16 tower, labelled,
 with its stated tolerance), tree_walk (select kernel, algorithmic bytes / time vs HBM peak),
-cpu_baseline (the oracle, rank 0, N=1, bounded sample), training (the C5 gradient step).
+c2_steady (configs[1] in steady state: 256 games, 6x64 f32, with its tower roofline),
+games_per_hr_measured (C2's games played to the end), cpu_baseline (the oracle, rank 0, N=1,
+bounded sample), training (the C5 gradient step, per-rank and sharded-batch modes).
 `--rehearse` runs the multi-rank plumbing with a CPU stub engine (no GPU; CI only).
 """
 import argparse
