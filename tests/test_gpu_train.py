@@ -336,6 +336,7 @@ def test_weight_grad_one_wave_per_simd_bit_identical(require_gpu, monkeypatch, b
     w = A.random_weights(blocks, 256, seed=19)
     planes, tpol, tval = batch(n, seed=400 + n)
     monkeypatch.setenv("AZ_TRAIN_WGRAD_COSPLIT", "0")
+    monkeypatch.setenv("AZ_TRAIN_WGRAD_COSPLIT4", "0")
     out = {}
     for flag in ("1", "0"):
         monkeypatch.setenv("AZ_TRAIN_WGRAD4", flag)
@@ -361,6 +362,7 @@ def test_weight_grad_output_channel_split_bit_identical(require_gpu, monkeypatch
     planes, tpol, tval = batch(n, seed=600 + n)
     monkeypatch.setenv("AZ_TRAIN_WGRAD_ROWS", str(rows))
     monkeypatch.setenv("AZ_TRAIN_WGRAD_COSPLIT", "0")
+    monkeypatch.setenv("AZ_TRAIN_WGRAD_COSPLIT4", "0")
     out = {}
     for flag in (str(n), "0"):
         monkeypatch.setenv(parts, flag)
