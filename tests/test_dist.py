@@ -81,6 +81,23 @@ def test_bench_gpus_flag_spawns_the_ranks():
     assert "2-way" in r["config"]["parallelism"]
 
 
+def test_bench_eight_ranks_c4_layout():
+    """configs[3] (C4: games sharded 8-way, no collective on the path) rehearsed on the CPU: `bench.py
+    --gpus 8` spawns 8 ranks over gloo with the stub engine (the driver's 8-GPU scaling run takes the
+    same code path with the real engine, one rank per GPU): one JSON line from rank 0, n_gpus = 8,
+    value = the simulations of all 8 ranks / the max-over-ranks time, 8 distinct game seeds."""
+    G, K, steps = 32, 8, 2
+    rc, lines, err = _bench(["--gpus", "8", "--rehearse", "--steps", str(steps), "--warmup", "1", "--games", str(G),
+                             "--sims", "16", "--sims-per-step", str(K), "--bf16-steps", "0", "--c2-steps", "0",
+                             "--games-leg", "0", "--train-steps", "0"], timeout=600)
+    assert rc == 0, err[-2000:]
+    assert len(lines) == 1
+    r = lines[0]
+    assert r["n_gpus"] == 8 and r["scaling"] == "weak" and "8-way" in r["config"]["parallelism"]
+    sims = r["value"] * r["ms_per_step"] * 1e-3 * steps
+    assert abs(sims - 8 * G * K * steps) < 1e-6 * sims
+
+
 def test_bench_rejects_world_mismatch():
     rc, lines, err = _bench(["--gpus", "1", "--rehearse", "--steps", "1"], env={"WORLD_SIZE": "2", "RANK": "0"})
     assert rc != 0 and not lines and "WORLD_SIZE=2" in err
