@@ -1339,6 +1339,9 @@ conv_wino_train_kernel(const float* __restrict__ X, const uint4* __restrict__ U,
 // Per chunk k (16 channels, 16 ring steps): the transform of chunk k + 1 (ACT slot (k + 1) & 1 ->
 // V[(k + 1) & 1]) early in the chunk, the staging of chunk k + 2 (global loads at the first step,
 // BatchNorm arithmetic + slot write at the last) into the slot chunk k left, one barrier.
+#ifndef AZ_PART_PF
+#define AZ_PART_PF 8      // ring prefetch steps of the quarter-channel kernel (one 16-channel block per wave)
+#endif
 #ifndef AZ_HALF_ISSUE
 #define AZ_HALF_ISSUE 0   // staging loads of chunk k + 2 at chunk k's first step (1: of chunk k + 3 at its last)
 #endif
@@ -1468,7 +1471,13 @@ conv_wino_part_kernel(const float* __restrict__ X, const uint4* __restrict__ U, 
     using namespace hk;
     constexpr int NB = 16 / (NP * NWV);                  // 16-channel output blocks per wave
     constexpr int SPI = NB == 1 ? 2 : 1;                 // ring steps per MFMA group
-    static_assert(NB * NP * NWV == 16 && SPX % SPI == 0, "part kernel config");
+    // weight-ring prefetch in steps: at NB = 1 a step is 4 MFMAs (128 cycles) of the SIMD's one
+    // wave, so 2 steps in flight left every ring wait short of the L2 latency (phase stamps: the
+    // core at 33 % of its MFMA bound, profiles/r06ab_trace64.txt).  64-position step: 6.45 / 5.72 /
+    // 5.16 / 5.35 ms at 2 / 4 / 8 / 16 steps (profiles/r06ac_*, r06ad_*), bit-identical.  (The
+    // halves' two blocks per wave at 4 steps: still behind the one-board kernel at 256; at 8 they spill.)
+    constexpr int PF = NB == 1 ? AZ_PART_PF : hk::PF;
+    static_assert(NB * NP * NWV == 16 && SPX % SPI == 0 && SPX % PF == 0, "part kernel config");
     __shared__ __attribute__((aligned(16))) uint4 lds[LDS_U4];
     char* const l = reinterpret_cast<char*>(lds);
     const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1951,8 +1960,8 @@ struct Trainer {
     int xev_used = 0;
     bool fuse_bn = true;                     // BN apply / backward staged in the next Winograd conv (env AZ_TRAIN_FUSE_BN=0: off)
     bool orc = true;                         // O's sign recomputed where no residual (env AZ_TRAIN_ORC=0: off)
-    int half = -1;                           // conv workgroups per board at small batches: -1 auto (4 when 4B <= the CU
-                                             // count, 2 when 2B <=), 0 one per board, 2 / 4 always (env AZ_TRAIN_HALF)
+    int half = -1;                           // conv workgroups per board at small batches: -1 auto (4 when B <= 192),
+                                             // 0 one per board, 2 / 4 always (env AZ_TRAIN_HALF)
     bool wgrad4 = true;                      // weight grad with one wave per SIMD (env AZ_TRAIN_WGRAD4=0: the 8-wave kernel)
     int wgrad_cosplit = 256;                 // batches up to this many boards split the one-wave weight grad's output
                                              // channels over two workgroups (env AZ_TRAIN_WGRAD_COSPLIT; round 6:
@@ -2010,8 +2019,8 @@ int launch_conv(Trainer* T, int taps, const float* X, int ldx, int K, const floa
 // the part kernel (NP workgroups per board) of launch_wino
 template <int NPART>
 int launch_wino_part(Trainer* T, const float* X, const uint4* U4, unsigned ub, const float* bias, const float* addend,
-                     float* Y, int B, int stats, tr::BoardStats bs, tr::BnIn bn, tr::BnBack bb) {
-    unsigned long long* htr = nullptr;
+                     float* Y, int B, int stats, tr::BoardStats bs, tr::BnIn bn, tr::BnBack bb,
+                     unsigned long long* htr) {   // phase stamps (trace build), one record per workgroup
     const unsigned g = (unsigned)(NPART * B);
     if (bn.out)
         tr::conv_wino_part_kernel<NPART, false, 1, 1><<<g, 256, 0, T->st>>>(X, U4, ub, bias, nullptr, Y, bs, bn, bb, B, htr);
@@ -2055,13 +2064,16 @@ int launch_wino(Trainer* T, const float* X, const float* U, const float* bias, c
     }
 #endif
     // small batches (the 512 / world shard of a sharded step): four quarter-channel workgroups per
-    // board when 2B <= 256 fill the CUs the one-board kernel leaves idle (conv_wino_part_kernel,
-    // bit-identical to it).  Step at B = 64: 6.78 ms against 7.90 (halves) and 8.93 (one board);
-    // B = 128: 8.24 / 8.93 / 9.87 (profiles/r06g_ab_parts_b*.txt); at B = 256 halves lose (12.37 vs
-    // 11.96, r06e)
-    const int np = T->half >= 0 ? T->half : (2 * B <= AZ_TRAIN_WG ? 4 : 0);
-    if (np == 2) return launch_wino_part<2>(T, X, U4, ub, bias, addend, Y, B, stats, bs, bn, bb);
-    if (np == 4) return launch_wino_part<4>(T, X, U4, ub, bias, addend, Y, B, stats, bs, bn, bb);
+    // board fill the CUs the one-board kernel leaves idle (conv_wino_part_kernel, bit-identical to
+    // it).  Step at B = 64: 6.78 ms against 7.90 (halves) and 8.93 (one board); B = 128: 8.24 /
+    // 8.93 / 9.87 (profiles/r06g_ab_parts_b*.txt); at B = 256 halves lose (12.37 vs 11.96, r06e).
+    // With the quarters' deeper weight-ring prefetch (AZ_PART_PF): 7.49 / 8.66 / 9.58 at 128, and
+    // 10.35 / 10.86 / 10.53 at 192, 12.90 / 12.06 / 11.60 at 256 (r06ad_ab_parts_b*.txt): quarters up
+    // to 4B <= 3 x the CU count (B <= 192)
+    const int np = T->half >= 0 ? T->half : (4 * B <= 3 * AZ_TRAIN_WG ? 4 : 0);
+    // (trace build: one record per workgroup; trb holds TRACE_BOARDS >= 4 x 128)
+    if (np == 2) return launch_wino_part<2>(T, X, U4, ub, bias, addend, Y, B, stats, bs, bn, bb, trb);
+    if (np == 4) return launch_wino_part<4>(T, X, U4, ub, bias, addend, Y, B, stats, bs, bn, bb, trb);
     if (np != 0) return fail("Winograd conv: AZ_TRAIN_HALF must be -1, 0, 2 or 4");
     const unsigned wg = (unsigned)std::min(B, AZ_TRAIN_WG);   // persistent workgroups (one per CU)
     // ORC: O's sign recomputed (no residual: BN 0 and BN1s) where the host asks for it

@@ -3,7 +3,8 @@ trace=-DAZ_TOWER_TRACE, run with AZ_LIB=build_var/trace/libaz.so): per launch of
 conv_wino_train_kernel in the last training step, the launch span and, per board (workgroup),
 staging (entry -> staged barrier), core (-> wino_core done), epilogue (-> exit), in shader clocks,
 and how busy the CUs were over the span.  20x256, batch 512, as tools/train_prof.py.
-Usage: AZ_LIB=... python tools/train_trace.py [steps]"""
+Usage: AZ_LIB=... python tools/train_trace.py [steps] [batch]   (batch <= 128: the part kernels, 4 or 2
+workgroups per board: NP x B records per launch)"""
 import ctypes as C
 import os
 import sys
@@ -14,7 +15,8 @@ import azchess as A
 from azchess import _lib as L
 
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
-B = 512
+B = int(sys.argv[2]) if len(sys.argv) > 2 else 512
+NP = 4 if 2 * B <= 256 else 1
 rng = np.random.default_rng(1)
 planes = (rng.random((B, 19, 64)) < 0.1).astype(np.float32)
 pol = rng.random((B, 4096)).astype(np.float32)
@@ -36,7 +38,7 @@ buf = np.zeros(NL * NB * 8, np.uint64)
 assert rd(buf.ctypes.data, buf.size, C.byref(n)) == 0
 buf = buf.reshape(NL, NB, 8).astype(np.int64)
 tot = {}
-NW = B                          # workgroups per launch (one board each)
+NW = NP * B                     # workgroups per launch (one board each, or NP parts of one)
 for k in range(counts[-1] - per_step, counts[-1]):
     t = buf[k % NL, :NW]
     # each XCD has its own shader clock: the span per XCD, the longest
@@ -71,6 +73,6 @@ for k in range(counts[-1] - per_step, counts[-1]):
     a += [span, stage.mean(), core.mean(), epi.mean(), 1]
 for ph, a in tot.items():
     s = a[:4] / a[4]
-    print("%s mean: span %.0f  stage %.0f (%.1f%%)  core %.0f (%.1f%%)  epi %.0f (%.1f%%)  [2 boards per CU: 2 x (stage+core+epi) = %.0f]"
+    print("%s mean: span %.0f  stage %.0f (%.1f%%)  core %.0f (%.1f%%)  epi %.0f (%.1f%%)  [2 x (stage+core+epi) = %.0f]"
           % (ph, s[0], s[1], 100 * s[1] / (s[1] + s[2] + s[3]), s[2], 100 * s[2] / (s[1] + s[2] + s[3]),
              s[3], 100 * s[3] / (s[1] + s[2] + s[3]), 2 * (s[1] + s[2] + s[3])))
