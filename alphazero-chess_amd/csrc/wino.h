@@ -99,10 +99,7 @@ constexpr int WINO_TSPLIT = 2, WINO_TSTAG = 16, WINO_LA = 4;
 template <int F> struct WinoCfg;
 template <> struct WinoCfg<256> { static constexpr int NWV = 8, NN = 2, XS = 1, CH = 32, PF = 2; };
 template <> struct WinoCfg<128> { static constexpr int NWV = 8, NN = 1, XS = 2, CH = 32, PF = 2; };
-#ifndef AZ_WINO64_PF
-#define AZ_WINO64_PF 2
-#endif
-template <> struct WinoCfg<64> { static constexpr int NWV = 4, NN = 1, XS = 2, CH = 64, PF = AZ_WINO64_PF; };
+template <> struct WinoCfg<64> { static constexpr int NWV = 4, NN = 1, XS = 2, CH = 64, PF = 2; };
 // Winograd weight fragment offsets: wave w's lane base (output fragments NN w..) and the byte
 // offset of ring step t (16-channel group kl = t / 16, point t % 16) of chunk cg
 template <int F> __device__ __forceinline__ int wino_voff(int w, int lane) {
