@@ -580,8 +580,15 @@ wino_wgrad_gemm4_kernel(const float* __restrict__ X, const float* __restrict__ D
 // out[e] = sum over splits s (in order) of partial[s][e]
 __global__ void reduce_kernel(const float* __restrict__ partial, int splits, size_t n, float* __restrict__ out) {
     for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
-        float s = 0.0f;
-        for (int k = 0; k < splits; k++) s += partial[(size_t)k * n + e];
+        float s = 0.0f;   // (the splits' loads 8 at a time, added in order: see wino_wgrad_reduce_out_kernel)
+        for (int k0 = 0; k0 < splits; k0 += 8) {
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) v[j] = partial[(size_t)min(k0 + j, splits - 1) * n + e];
+#pragma unroll
+            for (int j = 0; j < 8; j++)
+                if (k0 + j < splits) s += v[j];
+        }
         out[e] = s;
     }
 }
@@ -695,26 +702,115 @@ colsum4_kernel(const float* __restrict__ V, int ld, int C, int R, const float* _
 
 // sum the row-block partials of channel c, one wavefront per channel: lane l adds blocks
 // l, l + 64, ... in order, then a fixed butterfly over the lanes -- a fixed order (the step stays
-// bit-reproducible), 64 loads in flight instead of one dependent chain of nblk
-__device__ __forceinline__ float part_sum(const float* part, int nblk, int C, int c, int which, int lane) {
-    float s = 0.0f;
-    for (int b = lane; b < nblk; b += 64) s += part[((size_t)b * 2 + which) * C + c];
+// bit-reproducible), 64 loads in flight instead of one dependent chain of nblk.  Each lane's loads
+// go out 8 at a time and are added in block order after they land (round 6: the loop issued one
+// load per round trip -- 8 dependent L2 trips for 512 boards, most of these kernels' 8 us)
+constexpr int PSUM_BATCH = 8;
+// one chunk of a lane's blocks, b0 + 64 k for k < NK: all loads first (past the end: the last block,
+// loaded and not added), then the adds in block order
+template <int NW, int NK>
+__device__ __forceinline__ void part_chunk(const float* part, int nblk, int C, int c, const int (&which)[NW], int b0,
+                                           float (&s)[NW]) {
+    float v[NW][NK];
 #pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
-    return s;
+    for (int k = 0; k < NK; k++)
+#pragma unroll
+        for (int q = 0; q < NW; q++) v[q][k] = part[((size_t)min(b0 + 64 * k, nblk - 1) * 2 + which[q]) * C + c];
+#pragma unroll
+    for (int k = 0; k < NK; k++)
+#pragma unroll
+        for (int q = 0; q < NW; q++) s[q] = b0 + 64 * k < nblk ? s[q] + v[q][k] : s[q];
 }
-// one wavefront per channel: launch finalize_grid(C) blocks of 256 threads
-inline int finalize_grid(int C) { return (C * 64 + 255) / 256; }
-#define FIN_CHANNEL()                                                       \
-    const int c = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);    \
-    const int lane = threadIdx.x & 63;                                      \
-    if (c >= C) return
+// the butterfly s += shfl_xor(s, m), m = 32 .. 1, of a wavefront's 64 lanes, over the 64 lanes of
+// a channel in a finalize workgroup (FIN_CHANNEL) through LDS: level m adds lane l + m into lane l,
+// l < m -- lane 0's operands at every level, so the same bits (the butterfly leaves every lane with
+// lane 0's value: x + y = y + x exactly).  Every thread of the workgroup calls it.
+__device__ __forceinline__ float lane_butterfly(float s) {
+    __shared__ float red[64][17];
+    const int lane = threadIdx.x >> 4, j = threadIdx.x & 15;
+    __syncthreads();   // the previous call's readers are done
+    red[lane][j] = s;
+    __syncthreads();
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        if (lane < m) red[lane][j] = red[lane][j] + red[lane + m][j];
+        __syncthreads();
+    }
+    return red[0][j];
+}
+template <int NW>
+__device__ __forceinline__ void part_sums(const float* part, int nblk, int C, int c, const int (&which)[NW], int lane,
+                                          float (&s)[NW]) {
+#pragma unroll
+    for (int q = 0; q < NW; q++) s[q] = 0.0f;
+    if (nblk <= 64) part_chunk<NW, 1>(part, nblk, C, c, which, lane, s);
+    else
+        for (int b0 = lane; b0 < nblk; b0 += 64 * PSUM_BATCH) part_chunk<NW, PSUM_BATCH>(part, nblk, C, c, which, b0, s);
+#pragma unroll
+    for (int q = 0; q < NW; q++) s[q] = lane_butterfly(s[q]);
+}
+__device__ __forceinline__ float part_sum(const float* part, int nblk, int C, int c, int which, int lane) {
+    float s[1];
+    part_sums<1>(part, nblk, C, c, {which}, lane, s);
+    return s[0];
+}
+// BN forward statistics of channel c from per-board partials (BoardStats STATS 1): the sum S and
+// sum_b [M2_b + 64 (S_b / 64 - S / R)^2] (Chan et al.'s pairwise update, every board 64 rows), both
+// in part_sum's order.  Up to 512 boards from one set of loads (the mean's butterfly, then the
+// deviations from the same registers); more in two passes.
+template <int NK>
+__device__ __forceinline__ void board_stats_regs(const float* part, int nb, int C, int c, int R, int lane, float& s,
+                                                 float& m2) {
+    float vs[NK], vm[NK];
+#pragma unroll
+    for (int k = 0; k < NK; k++) {
+        const int b = min(lane + 64 * k, nb - 1);
+        vs[k] = part[((size_t)b * 2) * C + c];
+        vm[k] = part[((size_t)b * 2 + 1) * C + c];
+    }
+    s = 0.0f;
+#pragma unroll
+    for (int k = 0; k < NK; k++) s = lane + 64 * k < nb ? s + vs[k] : s;
+    s = lane_butterfly(s);
+    const float mu = s / (float)R;
+    m2 = 0.0f;
+#pragma unroll
+    for (int k = 0; k < NK; k++) {
+        const float d = vs[k] / 64.0f - mu;
+        const float t = m2 + (vm[k] + 64.0f * (d * d));
+        m2 = lane + 64 * k < nb ? t : m2;
+    }
+    m2 = lane_butterfly(m2);
+}
+__device__ __forceinline__ void board_stats(const float* part, int nb, int C, int c, int R, int lane, float& s, float& m2) {
+    if (nb <= 64) return board_stats_regs<1>(part, nb, C, c, R, lane, s, m2);
+    if (nb <= 64 * PSUM_BATCH) return board_stats_regs<PSUM_BATCH>(part, nb, C, c, R, lane, s, m2);
+    s = part_sum(part, nb, C, c, 0, lane);
+    const float mu = s / (float)R;
+    m2 = 0.0f;
+    for (int b = lane; b < nb; b += 64) {
+        const float d = part[((size_t)b * 2) * C + c] / 64.0f - mu;
+        m2 += part[((size_t)b * 2 + 1) * C + c] + 64.0f * (d * d);
+    }
+    m2 = lane_butterfly(m2);
+}
+// workgroup = 16 channels x 64 lanes (launch finalize_grid(C) blocks of FIN_THREADS): thread
+// (lane tid >> 4, channel 16 blockIdx.x + tid % 16), so that 16 neighbouring threads read one 64-byte
+// run of a partials row.  (Round 6: one wavefront per channel read 4 useful bytes per 64-byte line,
+// 16 lines per run; the step's batched bias sums took 32.6 us.)  Channels past C load channel C - 1
+// and write nothing; every thread reaches the butterflies' barriers.
+constexpr int FIN_THREADS = 1024;
+inline int finalize_grid(int C) { return (C + 15) / 16; }
+#define FIN_CHANNEL()                                                            \
+    const int lane = threadIdx.x >> 4;                                           \
+    const bool cown = (int)(16 * blockIdx.x + (threadIdx.x & 15)) < C;           \
+    const int c = min((int)(16 * blockIdx.x + (threadIdx.x & 15)), C - 1)
 
 // dst[c] = sum  (bias gradients)
 __global__ void finalize_sum_kernel(const float* __restrict__ part, int nblk, int C, float* __restrict__ dst) {
     FIN_CHANNEL();
     const float s = part_sum(part, nblk, C, c, 0, lane);
-    if (lane == 0) dst[c] = s;
+    if (lane == 0 && cown) dst[c] = s;
 }
 
 // the bias gradients of every BN-fed conv of the step in one launch (they are needed only by the
@@ -724,14 +820,14 @@ __global__ void finalize_sum_batched_kernel(const float* __restrict__ part, size
                                             const uint32_t* __restrict__ dst, float* __restrict__ g) {
     FIN_CHANNEL();
     const float s = part_sum(part + blockIdx.y * pstride, nblk, C, c, 0, lane);
-    if (lane == 0) g[dst[blockIdx.y] + c] = s;
+    if (lane == 0 && cown) g[dst[blockIdx.y] + c] = s;
 }
 
 // mean[c] = sum / R
 __global__ void finalize_mean_kernel(const float* __restrict__ part, int nblk, int C, int R, float* __restrict__ mean) {
     FIN_CHANNEL();
     const float s = part_sum(part, nblk, C, c, 0, lane);
-    if (lane == 0) mean[c] = s / (float)R;
+    if (lane == 0 && cown) mean[c] = s / (float)R;
 }
 
 // var = sum / R; std = sqrt(var + eps); running stats: rm = rm*0.9 + mean*0.1, rv = rv*0.9 + var*0.1
@@ -739,7 +835,7 @@ __global__ void finalize_var_kernel(const float* __restrict__ part, int nblk, in
                                     float* __restrict__ stdv, float* __restrict__ rmean, float* __restrict__ rvar) {
     FIN_CHANNEL();
     const float var = part_sum(part, nblk, C, c, 0, lane) / (float)R;
-    if (lane != 0) return;
+    if (lane != 0 || !cown) return;
     stdv[c] = sqrtf(var + 1e-5f);
     rmean[c] = rmean[c] * 0.9f + mean[c] * 0.1f;
     rvar[c] = rvar[c] * 0.9f + var * 0.1f;
@@ -750,8 +846,10 @@ __global__ void finalize_var_kernel(const float* __restrict__ part, int nblk, in
 __global__ void finalize_bnback_kernel(const float* __restrict__ part, int nblk, int C, float* __restrict__ dgamma,
                                        float* __restrict__ dbeta, float* __restrict__ slot = nullptr) {
     FIN_CHANNEL();
-    const float b = part_sum(part, nblk, C, c, 0, lane), g = part_sum(part, nblk, C, c, 1, lane);
-    if (lane == 0) {
+    float bg[2];
+    part_sums<2>(part, nblk, C, c, {0, 1}, lane, bg);
+    const float b = bg[0], g = bg[1];
+    if (lane == 0 && cown) {
         dbeta[c] = b;
         dgamma[c] = g;
         if (slot) {
@@ -766,15 +864,10 @@ __global__ void finalize_bnback_kernel(const float* __restrict__ part, int nblk,
 __global__ void bn_board_var_kernel(const float* __restrict__ part, int nb, int C, int R, float* __restrict__ mean,
                                     float* __restrict__ stdv, float* __restrict__ rmean, float* __restrict__ rvar) {
     FIN_CHANNEL();
-    const float mu = part_sum(part, nb, C, c, 0, lane) / (float)R;
-    float m2 = 0.0f;
-    for (int b = lane; b < nb; b += 64) {
-        const float d = part[((size_t)b * 2) * C + c] / 64.0f - mu;
-        m2 += part[((size_t)b * 2 + 1) * C + c] + 64.0f * (d * d);
-    }
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) m2 += __shfl_xor(m2, m, 64);
-    if (lane != 0) return;
+    float s, m2;
+    board_stats(part, nb, C, c, R, lane, s, m2);
+    const float mu = s / (float)R;
+    if (lane != 0 || !cown) return;
     const float var = m2 / (float)R;
     mean[c] = mu;
     stdv[c] = sqrtf(var + 1e-5f);
@@ -794,16 +887,9 @@ __global__ void bn_board_var_kernel(const float* __restrict__ part, int nb, int 
 __global__ void bn_local_kernel(const float* __restrict__ part, int nb, int C, int R, float* __restrict__ slot,
                                 int sstride) {
     FIN_CHANNEL();
-    const float s = part_sum(part, nb, C, c, 0, lane);
-    const float mu = s / (float)R;
-    float m2 = 0.0f;
-    for (int b = lane; b < nb; b += 64) {
-        const float d = part[((size_t)b * 2) * C + c] / 64.0f - mu;
-        m2 += part[((size_t)b * 2 + 1) * C + c] + 64.0f * (d * d);
-    }
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) m2 += __shfl_xor(m2, m, 64);
-    if (lane != 0) return;
+    float s, m2;
+    board_stats(part, nb, C, c, R, lane, s, m2);
+    if (lane != 0 || !cown) return;
     slot[c] = s;
     slot[sstride + c] = m2;
     if (c == 0) slot[2 * sstride] = (float)R;
@@ -860,10 +946,10 @@ void launch_colsum(dim3 g, hipStream_t st, const float* V, int ld, int C, int R,
     if (vec) colsum4_kernel<MODE><<<g, 256, 0, st>>>(V, ld, C, R, mean, stdv, O, Y, part);
     else colsum_kernel<MODE><<<g, 256, 0, st>>>(V, ld, C, R, mean, stdv, O, Y, part);
     const int nb = (int)g.x, fg = finalize_grid(C);
-    if (fin.kind == FIN_SUM) finalize_sum_kernel<<<fg, 256, 0, st>>>(part, nb, C, fin.a);
-    else if (fin.kind == FIN_MEAN) finalize_mean_kernel<<<fg, 256, 0, st>>>(part, nb, C, R, fin.a);
-    else if (fin.kind == FIN_VAR) finalize_var_kernel<<<fg, 256, 0, st>>>(part, nb, C, R, fin.mean, fin.a, fin.b, fin.c);
-    else finalize_bnback_kernel<<<fg, 256, 0, st>>>(part, nb, C, fin.a, fin.b);
+    if (fin.kind == FIN_SUM) finalize_sum_kernel<<<fg, FIN_THREADS, 0, st>>>(part, nb, C, fin.a);
+    else if (fin.kind == FIN_MEAN) finalize_mean_kernel<<<fg, FIN_THREADS, 0, st>>>(part, nb, C, R, fin.a);
+    else if (fin.kind == FIN_VAR) finalize_var_kernel<<<fg, FIN_THREADS, 0, st>>>(part, nb, C, R, fin.mean, fin.a, fin.b, fin.c);
+    else finalize_bnback_kernel<<<fg, FIN_THREADS, 0, st>>>(part, nb, C, fin.a, fin.b);
 }
 
 // ------------------------------------------------------------------ element-wise
@@ -1769,7 +1855,9 @@ __global__ void repack3x3_kernel(const float* __restrict__ w, int co_n, int ci_n
 // gradient's burn layout g[co][ci][3][3] (bit-identical to the round-3 reduce_kernel + separate
 // transform, 13.4 + 5.7 us per conv, without the dU round trip).  Workgroup = 64 lanes x 4
 // consecutive e x 16 waves, wave = point: each thread's split loads are independent 16-byte loads
-// (round 5: 13.9 us per conv against 15.5 with one e per lane, bit-identical; a 4 ci x 64 co tile
+// (round 5: 13.9 us per conv against 15.5 with one e per lane, bit-identical; round 6: the splits'
+// loads 16 at a time, 16.2 against 14.1 us -- the kernel is bandwidth-, not latency-bound (4.8 TB/s);
+// a 4 ci x 64 co tile
 // written as contiguous runs per co measured 23.4: too few workgroups), the points meet in LDS,
 // waves 0-11 = (element of the four, kernel row ky).  (Round 5: a 256-thread form -- which would
 // fit beside a Winograd conv workgroup on its CU -- on a second stream beside the next data-grad
@@ -2310,13 +2398,13 @@ int bn_forward(Trainer* T, int bi, const float* Y, int ld, int C, int R, size_t 
         float* my = T->xfwd + (size_t)T->rank * rs;
         if (bpart) {
             if (R % 64 || ld != C) return fail("bn: board statistics need whole boards");
-            tr::bn_local_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(bpart, R / 64, C, R, my, ss);
+            tr::bn_local_kernel<<<tr::finalize_grid(C), tr::FIN_THREADS, 0, T->st>>>(bpart, R / 64, C, R, my, ss);
         } else {   // the column sums of the unsharded path: S, the rank's mean, M2 about it
             const int nb = nblk_rows(R);
             dim3 g(nb, (C + 63) / 64);
             tr::launch_colsum<0>(g, T->st, Y, ld, C, R, nullptr, nullptr, nullptr, nullptr, T->cpart,
                                  {tr::FIN_SUM, my, nullptr, nullptr, nullptr});
-            tr::finalize_mean_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(T->cpart, nb, C, R, mean);
+            tr::finalize_mean_kernel<<<tr::finalize_grid(C), tr::FIN_THREADS, 0, T->st>>>(T->cpart, nb, C, R, mean);
             tr::launch_colsum<1>(g, T->st, Y, ld, C, R, mean, nullptr, nullptr, nullptr, T->cpart,
                                  {tr::FIN_SUM, my + ss, nullptr, nullptr, nullptr});
             tr::set_value_kernel<<<1, 1, 0, T->st>>>(my + 2 * ss, (float)R);
@@ -2326,7 +2414,7 @@ int bn_forward(Trainer* T, int bi, const float* Y, int ld, int C, int R, size_t 
                                                                  P + 3 * C, bi == 0 ? T->nglob : nullptr);
     } else if (bpart) {
         if (R % 64 || ld != C) return fail("bn: board statistics need whole boards");
-        tr::bn_board_var_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(bpart, R / 64, C, R, mean, sd, P + 2 * C,
+        tr::bn_board_var_kernel<<<tr::finalize_grid(C), tr::FIN_THREADS, 0, T->st>>>(bpart, R / 64, C, R, mean, sd, P + 2 * C,
                                                                         P + 3 * C);
     } else {
         const int nb = nblk_rows(R);
@@ -2352,7 +2440,7 @@ int bn_forward_heads_sharded(Trainer* T, int bi, int R, size_t poff, size_t voff
     dim3 g(nb, 1);
     tr::launch_colsum<0>(g, T->st, T->y40, 64, C, R, nullptr, nullptr, nullptr, nullptr, T->cpart,
                          {tr::FIN_SUM, my, nullptr, nullptr, nullptr});
-    tr::finalize_mean_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(T->cpart, nb, C, R, lmean);
+    tr::finalize_mean_kernel<<<tr::finalize_grid(C), tr::FIN_THREADS, 0, T->st>>>(T->cpart, nb, C, R, lmean);
     tr::launch_colsum<1>(g, T->st, T->y40, 64, C, R, lmean, nullptr, nullptr, nullptr, T->cpart,
                          {tr::FIN_SUM, my + ss, nullptr, nullptr, nullptr});
     tr::set_value_kernel<<<1, 1, 0, T->st>>>(my + 2 * ss, (float)R);
@@ -2388,7 +2476,7 @@ int bn_back_sums(Trainer* T, int bi, const float* dout, const float* O, const fl
     float* my = T->sharded && xchg ? T->xback + (size_t)T->rank * T->xbs : nullptr;
     if (bpart) {
         if (R % 64 || ld != C) return fail("bn: board statistics need whole boards");
-        tr::finalize_bnback_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(bpart, R / 64, C, dgam, dbet, my);
+        tr::finalize_bnback_kernel<<<tr::finalize_grid(C), tr::FIN_THREADS, 0, T->st>>>(bpart, R / 64, C, dgam, dbet, my);
     } else {
         const int nb = nblk_rows(R);
         dim3 g(nb, (C + 63) / 64);
@@ -2473,7 +2561,7 @@ int bn_back_apply(Trainer* T, int bi, const float* dout, const float* O, const f
         tr::bn_back4_kernel<<<g, 256, 0, T->st>>>(dout, O, Y, ld, C, R, mean, sd, T->p + bn_off, ug, ub, dy, dres,
                                                   bias ? bs : nullptr, nglob);
         if (batched) T->bias_pending[bi] = (int)g;
-        else if (bias) tr::finalize_sum_kernel<<<tr::finalize_grid(C), 256, 0, T->st>>>(T->bsum, (int)g, C, bias);
+        else if (bias) tr::finalize_sum_kernel<<<tr::finalize_grid(C), tr::FIN_THREADS, 0, T->st>>>(T->bsum, (int)g, C, bias);
     } else {
         tr::bn_back_kernel<<<grid_for((size_t)R * C), 256, 0, T->st>>>(dout, O, Y, ld, C, R, mean, sd, T->p + bn_off,
                                                                        ug, ub, dy, dres, nglob);
@@ -2588,7 +2676,7 @@ int trainer_grads(Trainer* T, const float* planes, const float* tpol, const floa
         const int nb = nblk_rows(B);
         dim3 g(nb, 2);
         tr::colsum_kernel<0><<<g, 256, 0, st>>>(T->vpart, 65, 65, B, nullptr, nullptr, nullptr, nullptr, T->cpart);
-        tr::finalize_sum_kernel<<<tr::finalize_grid(65), 256, 0, st>>>(T->cpart, nb, 65, T->dwtmp);
+        tr::finalize_sum_kernel<<<tr::finalize_grid(65), tr::FIN_THREADS, 0, st>>>(T->cpart, nb, 65, T->dwtmp);
         AZ_HIP(hipMemcpyAsync(T->g + L.l2w, T->dwtmp, 64 * sizeof(float), hipMemcpyDeviceToDevice, st));
         AZ_HIP(hipMemcpyAsync(T->g + L.l2b, T->dwtmp + 64, sizeof(float), hipMemcpyDeviceToDevice, st));
     }
@@ -2694,11 +2782,11 @@ int trainer_grads(Trainer* T, const float* planes, const float* tpol, const floa
         for (int j = 1; j < nt; j++) same = same && T->bias_pending[j] == T->bias_pending[1];
         const int j0 = same ? 1 : 0;
         if (same && T->bias_pending[1] > 0)
-            tr::finalize_sum_batched_kernel<<<dim3(tr::finalize_grid(F), nt - 1), 256, 0, st>>>(
+            tr::finalize_sum_batched_kernel<<<dim3(tr::finalize_grid(F), nt - 1), tr::FIN_THREADS, 0, st>>>(
                 T->bsum_all + T->bsum_stride, T->bsum_stride, T->bias_pending[1], F, T->bias_dst + 1, T->g);
         for (int j = same ? 0 : j0; j < (same ? 1 : nt); j++)
             if (T->bias_pending[j] > 0)
-                tr::finalize_sum_kernel<<<tr::finalize_grid(F), 256, 0, st>>>(
+                tr::finalize_sum_kernel<<<tr::finalize_grid(F), tr::FIN_THREADS, 0, st>>>(
                     T->bsum_all + (size_t)j * T->bsum_stride, T->bias_pending[j], F, T->g + L.tower[j].b);
         std::fill(T->bias_pending.begin(), T->bias_pending.end(), 0);
     }
