@@ -1856,7 +1856,7 @@ __global__ void repack3x3_kernel(const float* __restrict__ w, int co_n, int ci_n
 // transform, 13.4 + 5.7 us per conv, without the dU round trip).  Workgroup = 64 lanes x 4
 // consecutive e x 16 waves, wave = point: each thread's split loads are independent 16-byte loads
 // (round 5: 13.9 us per conv against 15.5 with one e per lane, bit-identical; round 6: the splits'
-// loads 16 at a time, 16.2 against 14.1 us -- the kernel is bandwidth-, not latency-bound (4.8 TB/s);
+// loads 2 / 4 / 16 at a time, 14.0 / 14.4 / 16.2 against 14.1 us -- bandwidth-, not latency-bound;
 // a 4 ci x 64 co tile
 // written as contiguous runs per co measured 23.4: too few workgroups), the points meet in LDS,
 // waves 0-11 = (element of the four, kernel row ky).  (Round 5: a 256-thread form -- which would
